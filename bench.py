@@ -1,0 +1,235 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X relay engine on BASELINE.json's headline workload.
+
+Metric (BASELINE.json): msg-edge relays/s (GTEPS) at 10M peers x 4096 msgs, 1-8 GPU, and % of
+the HBM roofline.  One relay = one Node.send_to_node call (p2pnetwork/node.py:114-116).
+
+Workload (default "c4" = BASELINE.json configs[3], the metric's own configuration): 10M-peer
+Barabasi-Albert (m=4) graph, 4096 concurrent push-gossip broadcasts with fanout 3 (Philox
+picks), synthetic graph and origins (no datasets).  A "step" = one complete broadcast: reset
+of the per-run state + every round until quiescence, graph resident in HBM.
+
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): broadcasts
+are independent, so each rank runs its own 4096 broadcasts (global message ids
+rank*4096 + m: different origins and Philox streams) on its own replica of the graph -- weak
+scaling with no data-path collective; value = relays of all ranks / max-over-ranks time.
+
+Prints ONE JSON line (rank 0) with the driver's fields plus "roofline" (dominant kernel,
+algorithmic bytes / its HIP-event time) and "cpu_baseline" (the C oracle on host cores).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "python-p2p-network_amd"))
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+
+WORKLOADS = {
+    "c4": dict(graph="ba", V=10_000_000, a=4, M=4096, mode="gossip", fanout=3,
+               name="config4: 10M-peer Barabasi-Albert m=4, 4096 push-gossip broadcasts, fanout 3"),
+    "c3": dict(graph="gnp", V=1_000_000, a=16, M=4096, mode="flood", fanout=3,
+               name="config3: 1M-peer Erdos-Renyi mean degree 16, 4096 flood broadcasts"),
+    "c2": dict(graph="rrg", V=1000, a=8, M=64, mode="flood", fanout=3,
+               name="config2: 1k-peer random 8-regular, 64 flood broadcasts"),
+}
+
+KCLASS = ("seed_update", "flood_pull", "gossip_scatter", "record")
+
+
+def model_bytes(rounds, mode):
+    """Algorithmic HBM bytes per kernel class for one run (DESIGN.md "byte model").
+
+    flood pull, round r:  8*wedges[r-1] + 8*words[r-1] + 4*degact[r-1]
+                                        + 8*peers[r-1] + 24*words[r]
+    gossip update, round r:             24*touched[r] (next read+clear, seen read)
+                                        + 16*words[r] (seen write, frontier write)
+    gossip scatter, round r:            8*words[r] + 8*peers[r] + 4*degact[r]
+                                        + 16*scatter[r] (read-modify-write of each pushed word)
+    """
+    b = {k: 0 for k in KCLASS}
+    for i, r in enumerate(rounds):
+        if mode == "flood":
+            if i >= 1:
+                p = rounds[i - 1]
+                b["flood_pull"] += (8 * p.wedges + 8 * p.active_words + 4 * p.deg_active
+                                    + 8 * p.active_vertices + 24 * r.active_words)
+        else:
+            if i >= 1:
+                b["seed_update"] += 24 * r.touched_words + 16 * r.active_words
+            b["gossip_scatter"] += (8 * r.active_words + 8 * r.active_vertices + 4 * r.deg_active
+                                    + 16 * r.scatter_words)
+    return b
+
+
+def survey_bytes(rounds, mode):
+    """SURVEY.md 8d reference model for the whole run (gossip: 8 B per bit relay)."""
+    tot = 0
+    for i, r in enumerate(rounds):
+        if i == 0:
+            continue
+        p = rounds[i - 1]
+        move = 8 * (p.wedges if mode == "flood" else p.relays)
+        tot += move + 8 * p.active_words + 4 * p.deg_active + 8 * p.active_vertices + 24 * r.active_words
+    return tot
+
+
+def build_graph(w):
+    from p2pnetwork.gpu import PeerGraph
+    if w["graph"] == "ba":
+        return PeerGraph.barabasi_albert(w["V"], int(w["a"]), seed=1)
+    if w["graph"] == "gnp":
+        return PeerGraph.gnp(w["V"], w["a"], seed=1)
+    if w["graph"] == "rrg":
+        return PeerGraph.random_regular(w["V"], int(w["a"]), seed=1)
+    raise ValueError(w["graph"])
+
+
+def cpu_baseline(g, w, src, sample_msgs):
+    """The C oracle (oracle/relay_oracle.c, OpenMP) on a bounded sample of the same workload:
+    the same graph with the first `sample_msgs` broadcasts.  Reported, not a target."""
+    from oracle import coracle
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    os.environ["OMP_NUM_THREADS"] = str(threads)
+    s = src[:sample_msgs]
+    t0 = time.perf_counter()
+    res = coracle.run(g.rowptr, g.colidx, s, w["mode"], w["fanout"], 0x5EED, 0, 0, 0, record=False)
+    dt = time.perf_counter() - t0
+    relays = sum(r["relays"] for r in res.rounds)
+    return {"value": relays / dt / 1e9, "unit": "GTEPS", "cores": threads, "kind": "port",
+            "sample": f"{sample_msgs} of {w['M']} broadcasts on the full {w['V']}-peer graph: "
+                      f"{relays} relays in {dt:.2f} s (oracle/relay_oracle.c, {threads} OpenMP threads)"}
+
+
+def load_traffic(workload, kernel):
+    """HBM traffic per launch of the dominant kernel from the committed rocprofv3 PMC pass
+    (profiles/traffic_<workload>.json, written by tools/pmc_traffic.py), if present."""
+    p = os.path.join(REPO, "profiles", f"traffic_{workload}.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        d = json.load(f)
+    return d.get("kernels", {}).get(kernel, {}).get("bytes_per_launch")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", default="c4", choices=sorted(WORKLOADS))
+    ap.add_argument("--cpu-sample-msgs", type=int, default=64)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from p2pnetwork.gpu import GraphNetwork, make_sources
+    w = WORKLOADS[args.workload]
+    t_gen = time.perf_counter()
+    g = build_graph(w)
+    t_gen = time.perf_counter() - t_gen
+    M = w["M"]
+    src = make_sources(g.V, M, seed=1, msg_id_base=rank * M)
+    net = GraphNetwork(g, mode=w["mode"], fanout=w["fanout"], gossip_seed=0x5EED, timing=True,
+                       device=local, msg_id_base=rank * M)
+    net.broadcast(src)
+    for _ in range(args.warmup):
+        net.reset()
+        net.run()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    barrier()
+    net.reset()  # zero the kernel timers; state re-zeroed again per step below
+    kt0 = net.kernel_times()
+    t0 = time.perf_counter()
+    relays = 0
+    all_rounds = []
+    for _ in range(args.steps):
+        net.reset()
+        rounds = net.run()
+        relays += sum(r.relays for r in rounds)
+        all_rounds.append(rounds)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    kt = net.kernel_times()  # reset() zeroes the timers: this is the LAST step's kernels
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        r = torch.tensor([relays], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(r, op=dist.ReduceOp.SUM)
+        relays = int(r.item())
+    del kt0
+
+    last = all_rounds[-1]
+    mb = model_bytes(last, w["mode"])
+    dominant = max(KCLASS, key=lambda k: kt[k][0])
+    dom_ms, dom_n = kt[dominant]
+    achieved = mb[dominant] / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
+    traffic = load_traffic(args.workload, dominant)
+    kernel_ms_total = sum(v[0] for v in kt.values())
+    out = {
+        "metric": "msg-edge relays/sec (GTEPS) at 10M peers x 4096 msgs; % HBM roofline",
+        "value": relays / elapsed / 1e9,
+        "unit": "GTEPS",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": "synthetic (generated graph + Philox origins)",
+        "config": {"workload": w["name"], "peers": g.V, "edges": g.n_edges, "broadcasts_per_gpu": M,
+                   "mode": w["mode"], "fanout": w["fanout"], "rounds": len(last),
+                   "parallelism": f"message-axis replicas x{world}" if world > 1 else "single GPU"},
+        "roofline": {
+            "bound": "hbm",
+            "kernel": dominant,
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBPS,
+            "traffic": traffic,
+            "algorithmic_bytes_per_launch": mb[dominant] / max(dom_n, 1),
+            "avg_launch_ms": dom_ms / max(dom_n, 1),
+            "launches_per_step": dom_n,
+        },
+        "kernel_ms_per_step": {k: v[0] for k, v in kt.items()},
+        "model_bytes_per_step": mb,
+        "whole_step_model_GBps": sum(mb.values()) / (elapsed / args.steps) / 1e9,
+        "survey_model_bytes_per_step": survey_bytes(last, w["mode"]),
+        "kernel_time_frac_of_step": kernel_ms_total / (elapsed / args.steps * 1e3),
+        "relays_per_step_per_gpu": relays / args.steps / world,
+        "graph_gen_s": t_gen,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(g, w, src, args.cpu_sample_msgs)
+    net.close()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

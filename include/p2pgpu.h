@@ -1,0 +1,133 @@
+/*
+ * p2pgpu.h -- C-ABI of the MI355X broadcast/relay engine (libp2pgpu.so).
+ *
+ * The engine replaces, for ONE hot path, what a p2pnetwork application does with
+ * Node.send_to_nodes + node_message + a message-id "seen" set (the dedup/no-echo contract of
+ * /root/reference/README.md:20): it runs that flood relay, and a push-gossip variant, over a
+ * whole simulated peer graph at once, 64 concurrent broadcasts per uint64 bitset word.
+ *
+ * Reference interface each entry point replaces (file:line in pj8912/python-p2p-network):
+ *   p2pg_load_csr / p2pg_graph_*  <- the topology built by Node.connect_with_node
+ *                                    (p2pnetwork/node.py:122-176); a peer's neighbour list is
+ *                                    Node.all_nodes = nodes_inbound + nodes_outbound (node.py:75-78)
+ *   p2pg_set_sources              <- the originating Node.send_to_nodes(data) call per broadcast
+ *                                    (node.py:106-112)
+ *   p2pg_step / p2pg_run          <- one / all rounds of: NodeConnection.run receive loop
+ *                                    (nodeconnection.py:186-218) -> Node.node_message
+ *                                    (node.py:334-338) -> app dedup -> send_to_nodes(data,
+ *                                    exclude=[sender]) (node.py:106-112) -> send_to_node
+ *                                    (node.py:114-120, message_count_send += 1 at :116)
+ *   p2pg_round_stats.relays       <- sum over peers of Node.message_count_send (node.py:65,116)
+ *   p2pg_get_new_deliveries       <- the node_message(node, data) events of one round, as
+ *                                    (peer, msg, hop, parent) records (node.py:334-338)
+ *   p2pg_read_planes              <- each app's "seen" set + first-receipt (hop, sender)
+ *   p2pg_last_error               <- (reference swallows errors via debug_print, node.py:80-83)
+ *
+ * Conventions: plain C types only; 0 = OK, negative = error (message via p2pg_last_error);
+ * no exceptions cross the ABI; the engine owns all device memory; caller keeps ownership of
+ * every host array it passes; one engine per host thread (not re-entrant).
+ */
+#ifndef P2PGPU_H
+#define P2PGPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define P2PG_OK 0
+#define P2PG_ERR_ARG (-1)
+#define P2PG_ERR_STATE (-2)
+#define P2PG_ERR_HIP (-3)
+#define P2PG_ERR_NOMEM (-4)
+#define P2PG_ERR_GRAPH (-5)
+
+#define P2PG_MODE_FLOOD 0  /* forward to all connections except the sender (node.py:106-112) */
+#define P2PG_MODE_GOSSIP 1 /* push-gossip: k Philox-chosen connections      */
+
+#define P2PG_FLAG_RECORD 1u /* keep hop/parent planes [V][M] (validation scale)            */
+#define P2PG_FLAG_TIMING 2u /* per-kernel HIP-event timing (p2pg_kernel_times)              */
+
+typedef struct p2pg_engine p2pg_engine;
+typedef struct p2pg_graph p2pg_graph;
+
+typedef struct p2pg_config {
+  int32_t mode;              /* P2PG_MODE_*                                              */
+  int32_t fanout;            /* gossip k (1..16); ignored for flood                       */
+  uint64_t gossip_seed;      /* Philox key for gossip picks                               */
+  uint64_t churn_seed;       /* Philox key for the per-round edge-drop mask               */
+  uint32_t churn_threshold;  /* send lost iff philox(...).x < threshold; 0 = no churn    */
+  uint32_t msg_id_base;      /* global id of local message 0 (message-axis sharding)      */
+  uint32_t flags;            /* P2PG_FLAG_*                                               */
+  int32_t device;            /* HIP device ordinal                                        */
+} p2pg_config;
+
+typedef struct p2pg_round_stats {
+  int32_t round;             /* round index r (0 = origination)                           */
+  int32_t active;            /* 1 if messages are still in flight after this round        */
+  uint64_t new_deliveries;   /* (peer,msg) first receipts in round r (= node_message events
+                                that pass dedup)                                          */
+  uint64_t relays;           /* send_to_node calls made in round r (message_count_send)   */
+  uint64_t active_vertices;  /* |A_r|: peers with >= 1 first receipt in round r           */
+  uint64_t active_words;     /* N_aw: nonzero (peer, word) of the round-r frontier        */
+  uint64_t wedges;           /* sum over nonzero frontier words of deg(peer)              */
+  uint64_t deg_active;       /* sum over A_r of deg(peer)                                 */
+  uint64_t scatter_words;    /* gossip: nonzero (sender, target, word) masks pushed       */
+  uint64_t touched_words;    /* gossip: nonzero pushed-to words consumed in round r       */
+} p2pg_round_stats;
+
+/* ---- graphs (host side; no GPU needed) ---------------------------------------------- */
+/* kind: 0 random d-regular (a = d), 1 G(n,p) with p = a / (V-1) (a = mean degree),
+ *       2 Barabasi-Albert (a = m, initial (m+1)-clique), 3 Watts-Strogatz (a = k, b = beta),
+ *       4 ring + chords (config 1: a = chord stride, 0 = none)                           */
+int p2pg_graph_generate(int32_t kind, int64_t V, double a, double b, uint64_t seed,
+                        p2pg_graph** out);
+/* Build from an undirected edge list (any order, duplicates/self-loops dropped). */
+int p2pg_graph_from_edges(int64_t V, int64_t n_edges, const int32_t* src, const int32_t* dst,
+                          p2pg_graph** out);
+int p2pg_graph_info(const p2pg_graph* g, int64_t* V, int64_t* nnz);
+/* Borrowed pointers, valid until p2pg_graph_free. */
+int p2pg_graph_arrays(const p2pg_graph* g, const int64_t** rowptr, const int32_t** colidx);
+void p2pg_graph_free(p2pg_graph* g);
+/* src[m] = lemire32(philox(key=(seed_lo, seed_hi ^ 'SRC'), ctr=(msg_id_base+m,0,0,0)).x, V) */
+int p2pg_make_sources(int64_t V, int32_t M, uint64_t seed, uint32_t msg_id_base, int32_t* src);
+/* Host Philox4x32-10 (KAT hook). */
+void p2pg_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
+
+/* ---- engine ------------------------------------------------------------------------- */
+int p2pg_create(const p2pg_config* cfg, p2pg_engine** out);
+int p2pg_load_csr(p2pg_engine* e, int64_t V, const int64_t* rowptr, const int32_t* colidx);
+int p2pg_set_sources(p2pg_engine* e, int32_t M, const int32_t* src);
+/* Back to round 0 with the same graph and sources (clears seen/frontier state). */
+int p2pg_reset(p2pg_engine* e);
+/* One round. Returns 1 while messages are in flight, 0 when quiescent, < 0 on error. */
+int p2pg_step(p2pg_engine* e, p2pg_round_stats* out);
+/* Rounds until quiescence or max_rounds; per_round may be NULL (else >= max_rounds slots). */
+int p2pg_run(p2pg_engine* e, int32_t max_rounds, p2pg_round_stats* per_round,
+             int32_t* n_rounds);
+/* The first receipts of the most recent round, sorted by (peer, msg); parent = -1 at the
+ * source.  Writes min(cap, count) records; *n_out = count (may exceed cap).             */
+int p2pg_get_new_deliveries(p2pg_engine* e, int64_t cap, int32_t* peer, int32_t* msg,
+                            int32_t* hop, int32_t* parent, int64_t* n_out);
+/* Validation copies: seen [V][W] uint64 (W = ceil(M/64)); hop/parent [V][M] int32 need
+ * P2PG_FLAG_RECORD (-1 = not delivered).  Any pointer may be NULL.                      */
+int p2pg_read_planes(p2pg_engine* e, uint64_t* seen, int32_t* hop, int32_t* parent);
+/* Summed device time per kernel class since the last reset (needs P2PG_FLAG_TIMING):
+ * ms[0] seed/update, ms[1] flood pull, ms[2] gossip scatter, ms[3] record/other;
+ * launches[i] likewise.                                                                 */
+int p2pg_kernel_times(p2pg_engine* e, double ms[4], int64_t launches[4]);
+/* Launch on this hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); NULL =
+ * the engine's own stream.                                                              */
+int p2pg_set_stream(p2pg_engine* e, void* hip_stream);
+/* Device-side Philox KAT: evaluates philox4x32_10 on n counters with one key.          */
+int p2pg_device_philox(p2pg_engine* e, int32_t n, const uint32_t* ctr, const uint32_t key[2],
+                       uint32_t* out);
+const char* p2pg_last_error(const p2pg_engine* e);
+const char* p2pg_global_error(void);
+void p2pg_destroy(p2pg_engine* e);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* P2PGPU_H */

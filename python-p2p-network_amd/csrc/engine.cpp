@@ -1,0 +1,530 @@
+// Host side of the relay engine: the C-ABI declared in include/p2pgpu.h.
+//
+// One engine = one GPU = one simulated peer graph resident in HBM.  Per round it launches a
+// handful of HIP kernels (relay_kernels.hip) on one stream and copies back 8 shards x 8
+// counters; nothing else crosses PCIe inside a run.
+//
+// Round schedule (r = round index; pushes made in round r arrive in round r+1):
+//   r = 0          seed: F[0], seen, A[0] <- source bits    (Node.send_to_nodes at the origin,
+//                                                            p2pnetwork/node.py:106-112)
+//   flood  r >= 1  pull:   F[r&1], A[r&1], seen <- OR of active neighbours' F[(r-1)&1]
+//   gossip r >= 1  update: F[r&1], A[r&1], seen <- next[r&1] & ~seen  (T[r&1] = touched rows)
+//   gossip r >= 0  scatter: next[(r+1)&1], T[(r+1)&1] |= k Philox picks of every F[r&1] bit
+//   record         hop/parent planes for the bits of F[r&1]   (P2PG_FLAG_RECORD only)
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "../../include/p2pgpu.h"
+#include "internal.h"
+
+using namespace p2pg;
+
+struct p2pg_engine {
+  p2pg_config cfg{};
+  std::string err;
+  int64_t V = 0, nnz = 0;
+  int32_t M = 0, W = 0;
+  std::vector<int64_t> h_rowptr;
+  std::vector<int32_t> h_src;
+  // device
+  int64_t* d_rowptr = nullptr;
+  int32_t* d_colidx = nullptr;
+  int64_t* d_hub = nullptr;
+  int64_t n_hub = 0;
+  int32_t* d_src = nullptr;
+  DevState st{};
+  size_t plane_bytes = 0, bm_bytes = 0;
+  unsigned long long* h_stats = nullptr;  // pinned
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  // per-launch timing events: recorded around each launch, resolved after the round's stream
+  // sync (no extra host synchronisation inside a round)
+  std::vector<hipEvent_t> ev_pool;
+  std::vector<int> ev_cls;  // class of pending pair i (events 2i, 2i+1)
+  double kms[4] = {0, 0, 0, 0};
+  int64_t klaunch[4] = {0, 0, 0, 0};
+  int32_t round = 0;
+  bool done = false;
+  bool have_state = false;
+};
+
+namespace {
+
+int fail(p2pg_engine* e, int code, const std::string& msg) {
+  if (e) e->err = msg;
+  set_global_error(msg);
+  return code;
+}
+
+#define HIPCHK(e, x)                                                                     \
+  do {                                                                                   \
+    hipError_t _r = (x);                                                                 \
+    if (_r != hipSuccess)                                                                \
+      return fail(e, P2PG_ERR_HIP, std::string(#x) + ": " + hipGetErrorString(_r));      \
+  } while (0)
+
+template <class T>
+void dfree(T*& p) {
+  if (p) (void)hipFree(p);
+  p = nullptr;
+}
+
+void free_state(p2pg_engine* e) {
+  DevState& s = e->st;
+  dfree(s.seen);
+  for (int i = 0; i < 2; ++i) {
+    dfree(s.F[i]);
+    dfree(s.next[i]);
+    dfree(s.A[i]);
+    dfree(s.T[i]);
+  }
+  dfree(s.S);
+  dfree(s.hop);
+  dfree(s.parent);
+  dfree(s.stats);
+  dfree(e->d_src);
+  e->have_state = false;
+}
+
+void free_graph(p2pg_engine* e) {
+  dfree(e->d_rowptr);
+  dfree(e->d_colidx);
+  dfree(e->d_hub);
+  e->n_hub = 0;
+}
+
+RoundParams params(const p2pg_engine* e) {
+  RoundParams p{};
+  p.round = e->round;
+  p.mode = e->cfg.mode;
+  p.fanout = e->cfg.fanout;
+  p.msg_base = e->cfg.msg_id_base;
+  p.gseed_lo = (uint32_t)e->cfg.gossip_seed;
+  p.gseed_hi = (uint32_t)(e->cfg.gossip_seed >> 32);
+  p.churn_thr = e->cfg.churn_threshold;
+  p.cseed_lo = (uint32_t)e->cfg.churn_seed;
+  p.cseed_hi = (uint32_t)(e->cfg.churn_seed >> 32);
+  return p;
+}
+
+DevGraph graph(const p2pg_engine* e) { return DevGraph{e->d_rowptr, e->d_colidx, e->V}; }
+
+// Timed launch: kernel class cls in [0,4).
+template <class F>
+int timed(p2pg_engine* e, int cls, F&& launch) {
+  const bool timing = (e->cfg.flags & P2PG_FLAG_TIMING) != 0;
+  size_t slot = 0;
+  if (timing) {
+    slot = e->ev_cls.size();
+    while (e->ev_pool.size() < 2 * (slot + 1)) {
+      hipEvent_t ev;
+      HIPCHK(e, hipEventCreate(&ev));
+      e->ev_pool.push_back(ev);
+    }
+    HIPCHK(e, hipEventRecord(e->ev_pool[2 * slot], e->stream));
+  }
+  hipError_t r = launch();
+  if (r != hipSuccess) return fail(e, P2PG_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString(r));
+  if (timing) {
+    HIPCHK(e, hipEventRecord(e->ev_pool[2 * slot + 1], e->stream));
+    e->ev_cls.push_back(cls);
+  }
+  e->klaunch[cls] += 1;
+  return P2PG_OK;
+}
+
+// After a stream sync: fold the pending launch timings into the per-class sums.
+int resolve_timings(p2pg_engine* e) {
+  for (size_t i = 0; i < e->ev_cls.size(); ++i) {
+    float ms = 0.f;
+    HIPCHK(e, hipEventElapsedTime(&ms, e->ev_pool[2 * i], e->ev_pool[2 * i + 1]));
+    e->kms[e->ev_cls[i]] += ms;
+  }
+  e->ev_cls.clear();
+  return P2PG_OK;
+}
+
+int alloc_state(p2pg_engine* e) {
+  free_state(e);
+  DevState& s = e->st;
+  s.W = e->W;
+  s.M = e->M;
+  e->plane_bytes = (size_t)e->V * e->W * sizeof(uint64_t);
+  e->bm_bytes = (size_t)((e->V + 31) / 32) * sizeof(uint32_t);
+  const bool gossip = e->cfg.mode == P2PG_MODE_GOSSIP;
+  const bool rec = (e->cfg.flags & P2PG_FLAG_RECORD) != 0;
+  auto A = [&](void** p, size_t n) -> int {
+    hipError_t r = hipMalloc(p, n ? n : 8);
+    if (r != hipSuccess) {
+      free_state(e);
+      return fail(e, r == hipErrorOutOfMemory ? P2PG_ERR_NOMEM : P2PG_ERR_HIP,
+                  std::string("hipMalloc: ") + hipGetErrorString(r));
+    }
+    return P2PG_OK;
+  };
+  int rc;
+  if ((rc = A((void**)&s.seen, e->plane_bytes))) return rc;
+  for (int i = 0; i < 2; ++i) {
+    if ((rc = A((void**)&s.F[i], e->plane_bytes))) return rc;
+    if ((rc = A((void**)&s.A[i], e->bm_bytes))) return rc;
+    if (gossip) {
+      if ((rc = A((void**)&s.next[i], e->plane_bytes))) return rc;
+      if ((rc = A((void**)&s.T[i], e->bm_bytes))) return rc;
+      HIPCHK(e, hipMemsetAsync(s.next[i], 0, e->plane_bytes, e->stream));
+      HIPCHK(e, hipMemsetAsync(s.T[i], 0, e->bm_bytes, e->stream));
+    }
+  }
+  if ((rc = A((void**)&s.S, e->bm_bytes))) return rc;
+  if (rec) {
+    const size_t hb = (size_t)e->V * e->M * sizeof(int32_t);
+    if ((rc = A((void**)&s.hop, hb))) return rc;
+    if ((rc = A((void**)&s.parent, hb))) return rc;
+  }
+  if ((rc = A((void**)&s.stats, sizeof(unsigned long long) * STAT_N * STAT_SHARDS))) return rc;
+  if ((rc = A((void**)&e->d_src, sizeof(int32_t) * (e->M ? e->M : 1)))) return rc;
+  e->have_state = true;
+  return P2PG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int p2pg_create(const p2pg_config* cfg, p2pg_engine** out) {
+  if (!cfg || !out) return fail(nullptr, P2PG_ERR_ARG, "create: null argument");
+  *out = nullptr;
+  if (cfg->mode != P2PG_MODE_FLOOD && cfg->mode != P2PG_MODE_GOSSIP)
+    return fail(nullptr, P2PG_ERR_ARG, "create: unknown mode");
+  if (cfg->mode == P2PG_MODE_GOSSIP && (cfg->fanout < 1 || cfg->fanout > 16))
+    return fail(nullptr, P2PG_ERR_ARG, "create: gossip fanout must be in [1, 16]");
+  int ndev = 0;
+  hipError_t r = hipGetDeviceCount(&ndev);
+  if (r != hipSuccess || ndev == 0)
+    return fail(nullptr, P2PG_ERR_HIP, "create: no HIP device visible");
+  if (cfg->device < 0 || cfg->device >= ndev)
+    return fail(nullptr, P2PG_ERR_ARG, "create: device ordinal out of range");
+  p2pg_engine* e = new p2pg_engine;
+  e->cfg = *cfg;
+  HIPCHK(e, hipSetDevice(cfg->device));
+  HIPCHK(e, hipStreamCreateWithFlags(&e->own_stream, hipStreamNonBlocking));
+  e->stream = e->own_stream;
+  HIPCHK(e, hipEventCreate(&e->ev[0]));
+  HIPCHK(e, hipEventCreate(&e->ev[1]));
+  HIPCHK(e, hipHostMalloc((void**)&e->h_stats,
+                          sizeof(unsigned long long) * STAT_N * STAT_SHARDS));
+  *out = e;
+  return P2PG_OK;
+}
+
+int p2pg_set_stream(p2pg_engine* e, void* hip_stream) {
+  if (!e) return P2PG_ERR_ARG;
+  e->stream = hip_stream ? (hipStream_t)hip_stream : e->own_stream;
+  return P2PG_OK;
+}
+
+int p2pg_load_csr(p2pg_engine* e, int64_t V, const int64_t* rowptr, const int32_t* colidx) {
+  if (!e || V <= 0 || V > 0x7FFFFFFFll || !rowptr) return fail(e, P2PG_ERR_ARG, "load_csr: bad arguments");
+  const int64_t nnz = rowptr[V];
+  if (rowptr[0] != 0 || nnz < 0 || (nnz > 0 && !colidx))
+    return fail(e, P2PG_ERR_GRAPH, "load_csr: rowptr[0] must be 0 and rowptr[V] >= 0");
+  // validate: monotone rows, ids in range, strictly ascending (sorted, no multi-edges),
+  // no self loops -- the invariants the kernels' lowest-id parent order relies on
+  for (int64_t v = 0; v < V; ++v) {
+    if (rowptr[v + 1] < rowptr[v]) return fail(e, P2PG_ERR_GRAPH, "load_csr: rowptr not monotone");
+    for (int64_t j = rowptr[v]; j < rowptr[v + 1]; ++j) {
+      const int32_t u = colidx[j];
+      if (u < 0 || u >= V) return fail(e, P2PG_ERR_GRAPH, "load_csr: neighbour id out of range");
+      if (u == v) return fail(e, P2PG_ERR_GRAPH, "load_csr: self loop");
+      if (j > rowptr[v] && colidx[j - 1] >= u)
+        return fail(e, P2PG_ERR_GRAPH, "load_csr: row not strictly ascending");
+    }
+  }
+  HIPCHK(e, hipSetDevice(e->cfg.device));
+  free_graph(e);
+  free_state(e);
+  e->V = V;
+  e->nnz = nnz;
+  e->h_rowptr.assign(rowptr, rowptr + V + 1);
+  HIPCHK(e, hipMalloc((void**)&e->d_rowptr, sizeof(int64_t) * (V + 1)));
+  HIPCHK(e, hipMalloc((void**)&e->d_colidx, sizeof(int32_t) * (nnz ? nnz : 1)));
+  HIPCHK(e, hipMemcpy(e->d_rowptr, rowptr, sizeof(int64_t) * (V + 1), hipMemcpyHostToDevice));
+  if (nnz) HIPCHK(e, hipMemcpy(e->d_colidx, colidx, sizeof(int32_t) * nnz, hipMemcpyHostToDevice));
+  // gossip: (source, neighbour-chunk) items for sources wider than one chunk
+  std::vector<int64_t> hub;
+  for (int64_t v = 0; v < V; ++v) {
+    const int64_t d = rowptr[v + 1] - rowptr[v];
+    if (d > GCHUNK)
+      for (int64_t c = 0; c * GCHUNK < d; ++c) hub.push_back((v << 32) | c);
+  }
+  e->n_hub = (int64_t)hub.size();
+  HIPCHK(e, hipMalloc((void**)&e->d_hub, sizeof(int64_t) * (hub.empty() ? 1 : hub.size())));
+  if (!hub.empty())
+    HIPCHK(e, hipMemcpy(e->d_hub, hub.data(), sizeof(int64_t) * hub.size(), hipMemcpyHostToDevice));
+  e->M = 0;
+  e->W = 0;
+  e->round = 0;
+  e->done = true;
+  return P2PG_OK;
+}
+
+int p2pg_set_sources(p2pg_engine* e, int32_t M, const int32_t* src) {
+  if (!e || M <= 0 || !src) return fail(e, P2PG_ERR_ARG, "set_sources: need M > 0 and src");
+  if (!e->d_rowptr) return fail(e, P2PG_ERR_STATE, "set_sources: load a graph first");
+  for (int32_t m = 0; m < M; ++m)
+    if (src[m] < 0 || src[m] >= e->V) return fail(e, P2PG_ERR_ARG, "set_sources: source out of range");
+  HIPCHK(e, hipSetDevice(e->cfg.device));
+  const int32_t W = (M + 63) / 64;
+  e->h_src.assign(src, src + M);
+  if (!e->have_state || W != e->W || M != e->M) {
+    e->M = M;
+    e->W = W;
+    int rc = alloc_state(e);
+    if (rc) return rc;
+  }
+  HIPCHK(e, hipMemcpy(e->d_src, src, sizeof(int32_t) * M, hipMemcpyHostToDevice));
+  return p2pg_reset(e);
+}
+
+int p2pg_reset(p2pg_engine* e) {
+  if (!e || !e->have_state) return fail(e, P2PG_ERR_STATE, "reset: no sources set");
+  HIPCHK(e, hipSetDevice(e->cfg.device));
+  DevState& s = e->st;
+  HIPCHK(e, hipMemsetAsync(s.seen, 0, e->plane_bytes, e->stream));
+  HIPCHK(e, hipMemsetAsync(s.S, 0, e->bm_bytes, e->stream));
+  for (int i = 0; i < 2; ++i) HIPCHK(e, hipMemsetAsync(s.A[i], 0, e->bm_bytes, e->stream));
+  if (e->cfg.mode == P2PG_MODE_GOSSIP && !e->done && e->round > 0) {
+    // an interrupted gossip run may leave pushes in flight: clear them
+    for (int i = 0; i < 2; ++i) {
+      HIPCHK(e, hipMemsetAsync(s.next[i], 0, e->plane_bytes, e->stream));
+      HIPCHK(e, hipMemsetAsync(s.T[i], 0, e->bm_bytes, e->stream));
+    }
+  }
+  if (s.hop) {
+    HIPCHK(e, hipMemsetAsync(s.hop, 0xFF, (size_t)e->V * e->M * sizeof(int32_t), e->stream));
+    HIPCHK(e, hipMemsetAsync(s.parent, 0xFF, (size_t)e->V * e->M * sizeof(int32_t), e->stream));
+  }
+  e->round = 0;
+  e->done = false;
+  for (int i = 0; i < 4; ++i) {
+    e->kms[i] = 0;
+    e->klaunch[i] = 0;
+  }
+  return P2PG_OK;
+}
+
+int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
+  if (!e || !e->have_state) return fail(e, P2PG_ERR_STATE, "step: no sources set");
+  if (e->done) {
+    if (out) {
+      std::memset(out, 0, sizeof(*out));
+      out->round = e->round;
+    }
+    return 0;
+  }
+  HIPCHK(e, hipSetDevice(e->cfg.device));
+  DevState& s = e->st;
+  const DevGraph g = graph(e);
+  const RoundParams p = params(e);
+  const bool gossip = e->cfg.mode == P2PG_MODE_GOSSIP;
+  HIPCHK(e, hipMemsetAsync(s.stats, 0, sizeof(unsigned long long) * STAT_N * STAT_SHARDS, e->stream));
+  int rc;
+  uint64_t host_new = 0, host_relays = 0, host_av = 0, host_aw = 0, host_wedge = 0, host_degact = 0;
+  if (e->round == 0) {
+    if ((rc = timed(e, 0, [&] { return launch_zero_rows(s.F[0], e->W, e->d_src, e->M, e->stream); }))) return rc;
+    if ((rc = timed(e, 0, [&] { return launch_seed(s, e->d_src, e->M, e->stream); }))) return rc;
+    // origination stats from the host copy of the sources
+    std::vector<int64_t> vs(e->h_src.begin(), e->h_src.end());
+    std::vector<int64_t> vw(e->M);
+    for (int32_t m = 0; m < e->M; ++m) {
+      const int64_t v = e->h_src[m];
+      const int64_t d = e->h_rowptr[v + 1] - e->h_rowptr[v];
+      host_relays += gossip ? (uint64_t)std::min<int64_t>(d, e->cfg.fanout) : (uint64_t)d;
+      vw[m] = v * e->W + (m >> 6);
+    }
+    host_new = (uint64_t)e->M;
+    std::sort(vs.begin(), vs.end());
+    vs.erase(std::unique(vs.begin(), vs.end()), vs.end());
+    std::sort(vw.begin(), vw.end());
+    vw.erase(std::unique(vw.begin(), vw.end()), vw.end());
+    host_av = vs.size();
+    host_aw = vw.size();
+    for (int64_t v : vs) host_degact += (uint64_t)(e->h_rowptr[v + 1] - e->h_rowptr[v]);
+    for (int64_t x : vw) {
+      const int64_t v = x / e->W;
+      host_wedge += (uint64_t)(e->h_rowptr[v + 1] - e->h_rowptr[v]);
+    }
+  } else if (!gossip) {
+    if ((rc = timed(e, 1, [&] { return launch_flood_pull(g, s, p, e->stream); }))) return rc;
+  } else {
+    if ((rc = timed(e, 0, [&] { return launch_gossip_update(g, s, p, e->stream); }))) return rc;
+  }
+  if (s.hop)
+    if ((rc = timed(e, 3, [&] { return launch_record(g, s, p, e->stream); }))) return rc;
+  if (gossip)
+    if ((rc = timed(e, 2, [&] {
+           return launch_gossip_scatter(g, s, p, e->d_hub, e->n_hub, e->stream);
+         })))
+      return rc;
+  HIPCHK(e, hipMemcpyAsync(e->h_stats, s.stats, sizeof(unsigned long long) * STAT_N * STAT_SHARDS,
+                           hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  if ((rc = resolve_timings(e))) return rc;
+  uint64_t tot[STAT_N] = {0};
+  for (int sh = 0; sh < STAT_SHARDS; ++sh)
+    for (int i = 0; i < STAT_N; ++i) tot[i] += e->h_stats[sh * STAT_N + i];
+  if (e->round == 0) {
+    tot[ST_NEW] = host_new;
+    tot[ST_RELAYS] = host_relays;
+    tot[ST_ACTIVE_V] = host_av;
+    tot[ST_ACTIVE_W] = host_aw;
+    tot[ST_WEDGES] = host_wedge;
+    tot[ST_DEG_ACT] = host_degact;
+  }
+  const bool active = tot[ST_NEW] != 0;
+  if (out) {
+    out->round = e->round;
+    out->active = active ? 1 : 0;
+    out->new_deliveries = tot[ST_NEW];
+    out->relays = tot[ST_RELAYS];
+    out->active_vertices = tot[ST_ACTIVE_V];
+    out->active_words = tot[ST_ACTIVE_W];
+    out->wedges = tot[ST_WEDGES];
+    out->deg_active = tot[ST_DEG_ACT];
+    out->scatter_words = tot[ST_SCATTER];
+    out->touched_words = tot[ST_AUX];
+  }
+  e->round += 1;
+  if (!active) e->done = true;
+  return active ? 1 : 0;
+}
+
+int p2pg_run(p2pg_engine* e, int32_t max_rounds, p2pg_round_stats* per_round,
+             int32_t* n_rounds) {
+  if (!e) return P2PG_ERR_ARG;
+  int32_t n = 0;
+  int rc = 1;
+  while (n < max_rounds) {
+    p2pg_round_stats tmp;
+    rc = p2pg_step(e, per_round ? &per_round[n] : &tmp);
+    if (rc < 0) return rc;
+    ++n;
+    if (rc == 0) break;
+  }
+  if (n_rounds) *n_rounds = n;
+  return rc;
+}
+
+int p2pg_get_new_deliveries(p2pg_engine* e, int64_t cap, int32_t* peer, int32_t* msg,
+                            int32_t* hop, int32_t* parent, int64_t* n_out) {
+  if (!e || cap < 0 || !n_out || (cap > 0 && (!peer || !msg || !hop || !parent)))
+    return fail(e, P2PG_ERR_ARG, "get_new_deliveries: bad arguments");
+  if (!e->have_state || e->round == 0)
+    return fail(e, P2PG_ERR_STATE, "get_new_deliveries: no round has run");
+  HIPCHK(e, hipSetDevice(e->cfg.device));
+  // the most recent round is e->round - 1; its frontier is F[(round-1)&1]
+  RoundParams p = params(e);
+  p.round = e->round - 1;
+  const DevGraph g = graph(e);
+  int32_t *dpeer = nullptr, *dmsg = nullptr, *dpar = nullptr;
+  unsigned long long* dcnt = nullptr;
+  const int64_t c = cap > 0 ? cap : 1;
+  HIPCHK(e, hipMalloc((void**)&dpeer, sizeof(int32_t) * c));
+  HIPCHK(e, hipMalloc((void**)&dmsg, sizeof(int32_t) * c));
+  HIPCHK(e, hipMalloc((void**)&dpar, sizeof(int32_t) * c));
+  HIPCHK(e, hipMalloc((void**)&dcnt, sizeof(unsigned long long)));
+  HIPCHK(e, hipMemsetAsync(dcnt, 0, sizeof(unsigned long long), e->stream));
+  hipError_t lr = launch_deliveries(g, e->st, p, cap, dpeer, dmsg, dpar, dcnt, e->stream);
+  unsigned long long cnt = 0;
+  if (lr == hipSuccess) lr = hipMemcpyAsync(&cnt, dcnt, sizeof(cnt), hipMemcpyDeviceToHost, e->stream);
+  if (lr == hipSuccess) lr = hipStreamSynchronize(e->stream);
+  const int64_t n = std::min<int64_t>((int64_t)cnt, cap);
+  std::vector<int32_t> hp(n), hm(n), hpar(n);
+  if (lr == hipSuccess && n > 0) {
+    lr = hipMemcpy(hp.data(), dpeer, sizeof(int32_t) * n, hipMemcpyDeviceToHost);
+    if (lr == hipSuccess) lr = hipMemcpy(hm.data(), dmsg, sizeof(int32_t) * n, hipMemcpyDeviceToHost);
+    if (lr == hipSuccess) lr = hipMemcpy(hpar.data(), dpar, sizeof(int32_t) * n, hipMemcpyDeviceToHost);
+  }
+  (void)hipFree(dpeer);
+  (void)hipFree(dmsg);
+  (void)hipFree(dpar);
+  (void)hipFree(dcnt);
+  if (lr != hipSuccess) return fail(e, P2PG_ERR_HIP, std::string("get_new_deliveries: ") + hipGetErrorString(lr));
+  // deterministic order: ascending (peer, msg)  (the compat layer replays hooks in it)
+  std::vector<int64_t> idx(n);
+  std::iota(idx.begin(), idx.end(), 0);
+  std::sort(idx.begin(), idx.end(), [&](int64_t a, int64_t b) {
+    return hp[a] != hp[b] ? hp[a] < hp[b] : hm[a] < hm[b];
+  });
+  for (int64_t i = 0; i < n; ++i) {
+    peer[i] = hp[idx[i]];
+    msg[i] = hm[idx[i]];
+    hop[i] = p.round;
+    parent[i] = hpar[idx[i]];
+  }
+  *n_out = (int64_t)cnt;
+  return P2PG_OK;
+}
+
+int p2pg_read_planes(p2pg_engine* e, uint64_t* seen, int32_t* hop, int32_t* parent) {
+  if (!e || !e->have_state) return fail(e, P2PG_ERR_STATE, "read_planes: no state");
+  if ((hop || parent) && !e->st.hop)
+    return fail(e, P2PG_ERR_STATE, "read_planes: hop/parent need P2PG_FLAG_RECORD");
+  HIPCHK(e, hipSetDevice(e->cfg.device));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  if (seen) HIPCHK(e, hipMemcpy(seen, e->st.seen, e->plane_bytes, hipMemcpyDeviceToHost));
+  const size_t hb = (size_t)e->V * e->M * sizeof(int32_t);
+  if (hop) HIPCHK(e, hipMemcpy(hop, e->st.hop, hb, hipMemcpyDeviceToHost));
+  if (parent) HIPCHK(e, hipMemcpy(parent, e->st.parent, hb, hipMemcpyDeviceToHost));
+  return P2PG_OK;
+}
+
+int p2pg_kernel_times(p2pg_engine* e, double ms[4], int64_t launches[4]) {
+  if (!e) return P2PG_ERR_ARG;
+  for (int i = 0; i < 4; ++i) {
+    if (ms) ms[i] = e->kms[i];
+    if (launches) launches[i] = e->klaunch[i];
+  }
+  return P2PG_OK;
+}
+
+int p2pg_device_philox(p2pg_engine* e, int32_t n, const uint32_t* ctr, const uint32_t key[2],
+                       uint32_t* out) {
+  if (!e || n < 0 || (n > 0 && (!ctr || !key || !out))) return fail(e, P2PG_ERR_ARG, "device_philox: bad arguments");
+  if (n == 0) return P2PG_OK;
+  HIPCHK(e, hipSetDevice(e->cfg.device));
+  uint32_t *dc = nullptr, *dout = nullptr;
+  HIPCHK(e, hipMalloc((void**)&dc, sizeof(uint32_t) * 4 * n));
+  HIPCHK(e, hipMalloc((void**)&dout, sizeof(uint32_t) * 4 * n));
+  hipError_t r = hipMemcpy(dc, ctr, sizeof(uint32_t) * 4 * n, hipMemcpyHostToDevice);
+  if (r == hipSuccess) r = launch_philox(n, dc, key[0], key[1], dout, e->stream);
+  if (r == hipSuccess) r = hipStreamSynchronize(e->stream);
+  if (r == hipSuccess) r = hipMemcpy(out, dout, sizeof(uint32_t) * 4 * n, hipMemcpyDeviceToHost);
+  (void)hipFree(dc);
+  (void)hipFree(dout);
+  if (r != hipSuccess) return fail(e, P2PG_ERR_HIP, std::string("device_philox: ") + hipGetErrorString(r));
+  return P2PG_OK;
+}
+
+const char* p2pg_last_error(const p2pg_engine* e) { return e ? e->err.c_str() : p2pg_global_error(); }
+
+void p2pg_destroy(p2pg_engine* e) {
+  if (!e) return;
+  (void)hipSetDevice(e->cfg.device);
+  (void)hipStreamSynchronize(e->stream);
+  free_state(e);
+  free_graph(e);
+  if (e->h_stats) (void)hipHostFree(e->h_stats);
+  for (int i = 0; i < 2; ++i)
+    if (e->ev[i]) (void)hipEventDestroy(e->ev[i]);
+  for (hipEvent_t ev : e->ev_pool) (void)hipEventDestroy(ev);
+  if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
+  delete e;
+}
+
+}  // extern "C"

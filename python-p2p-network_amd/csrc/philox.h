@@ -1,0 +1,117 @@
+// Philox4x32-10 counter-based RNG, shared by host (generators, sources) and device (gossip
+// picks, churn mask) so that every random decision is a pure function of its counter.
+//
+// Constants: Salmon et al., "Parallel random numbers: as easy as 1, 2, 3" (SC'11) /
+// Random123; same values as /opt/rocm/include/rocrand/rocrand_philox4x32_10.h:62-65.
+// Known-answer vectors (Random123 kat_vectors) are pinned in tests/test_philox.py.
+//
+// Counter layouts used by the engine:
+//   sources : key = (seed_lo, seed_hi ^ TAG_SRC), ctr = (msg_global, 0, 0, 0)
+//   gossip  : key = (seed_lo, seed_hi),           ctr = (round, peer, msg_global, TAG_GSP | blk<<24)
+//   churn   : key = (seed_lo, seed_hi),           ctr = (round, min(a,b), max(a,b), TAG_CHN)
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define P2PG_HD __host__ __device__ __forceinline__
+#else
+#define P2PG_HD static inline
+#endif
+
+namespace p2pg {
+
+constexpr uint32_t PHILOX_M0 = 0xD2511F53u;
+constexpr uint32_t PHILOX_M1 = 0xCD9E8D57u;
+constexpr uint32_t PHILOX_W0 = 0x9E3779B9u;
+constexpr uint32_t PHILOX_W1 = 0xBB67AE85u;
+
+constexpr uint32_t TAG_SRC = 0x00535243u;  // 'SRC'
+constexpr uint32_t TAG_GSP = 0x00475350u;  // 'GSP'
+constexpr uint32_t TAG_CHN = 0x0043484Eu;  // 'CHN'
+constexpr uint32_t TAG_RRG = 0x00525247u;  // 'RRG' random-regular generator
+constexpr uint32_t TAG_GNP = 0x00474E50u;  // 'GNP'
+constexpr uint32_t TAG_BAG = 0x00424147u;  // 'BAG' Barabasi-Albert generator
+constexpr uint32_t TAG_WSG = 0x00575347u;  // 'WSG' Watts-Strogatz generator
+
+struct u32x4 { uint32_t x, y, z, w; };
+
+P2PG_HD u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
+  // 32x32->64 products as one 64-bit multiply: lowers to v_mad_u64_u32 on gfx950, which the
+  // microbenchmark (tools/microbench/philox_rate.hip) measured 1.3x faster than mul_hi+mul_lo.
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const uint64_t p0 = (uint64_t)PHILOX_M0 * c.x;
+    const uint64_t p1 = (uint64_t)PHILOX_M1 * c.z;
+    u32x4 n;
+    n.x = (uint32_t)(p1 >> 32) ^ c.y ^ k0;
+    n.y = (uint32_t)p1;
+    n.z = (uint32_t)(p0 >> 32) ^ c.w ^ k1;
+    n.w = (uint32_t)p0;
+    c = n;
+    k0 += PHILOX_W0;
+    k1 += PHILOX_W1;
+  }
+  return c;
+}
+
+// Lemire multiply-high reduction of a 32-bit draw onto [0, n).
+P2PG_HD uint32_t lemire32(uint32_t x, uint32_t n) {
+  return (uint32_t)(((uint64_t)x * (uint64_t)n) >> 32);
+}
+
+P2PG_HD uint32_t word_of(const u32x4& r, int i) {
+  return i == 0 ? r.x : (i == 1 ? r.y : (i == 2 ? r.z : r.w));
+}
+
+// Push-gossip target choice: k distinct indices into the sender's ascending
+// adjacency list of length n, by Floyd's algorithm; draw i uses word (i % 4) of Philox block
+// (i / 4).  Requires n > k (callers send to every neighbour when n <= k).  Writes the k
+// picks to out[0..k) in draw order.  K_MAX bounds the storage of the caller.
+P2PG_HD void gossip_picks(uint32_t round, uint32_t peer, uint32_t msg, uint32_t n, int k,
+                          uint32_t seed_lo, uint32_t seed_hi, uint32_t* out) {
+  u32x4 r = {0, 0, 0, 0};
+  for (int i = 0; i < k; ++i) {
+    if ((i & 3) == 0) {
+      u32x4 c = {round, peer, msg, TAG_GSP | ((uint32_t)(i >> 2) << 24)};
+      r = philox4x32_10(c, seed_lo, seed_hi);
+    }
+    const uint32_t jmax = n - (uint32_t)k + (uint32_t)i;  // Floyd: candidate range [0, jmax]
+    uint32_t t = lemire32(word_of(r, i & 3), jmax + 1u);
+    bool dup = false;
+    for (int q = 0; q < i; ++q) dup |= (out[q] == t);
+    out[i] = dup ? jmax : t;
+  }
+}
+
+// Same draws with k fixed at compile time, so out[] stays in registers on the device (a
+// runtime-indexed private array would live in scratch memory).
+template <int K>
+P2PG_HD void gossip_picks_t(uint32_t round, uint32_t peer, uint32_t msg, uint32_t n,
+                            uint32_t seed_lo, uint32_t seed_hi, uint32_t (&out)[K]) {
+  u32x4 r = {0, 0, 0, 0};
+#pragma unroll
+  for (int i = 0; i < K; ++i) {
+    if ((i & 3) == 0) {
+      u32x4 c = {round, peer, msg, TAG_GSP | ((uint32_t)(i >> 2) << 24)};
+      r = philox4x32_10(c, seed_lo, seed_hi);
+    }
+    const uint32_t jmax = n - (uint32_t)K + (uint32_t)i;
+    const uint32_t t = lemire32(word_of(r, i & 3), jmax + 1u);
+    bool dup = false;
+#pragma unroll
+    for (int q = 0; q < i; ++q) dup |= (out[q] == t);
+    out[i] = dup ? jmax : t;
+  }
+}
+
+// Churn: a send over undirected edge {a,b} made in round r is lost iff the
+// first Philox word is below the threshold floor(p_drop * 2^32).
+P2PG_HD bool churn_dropped(uint32_t round, uint32_t a, uint32_t b, uint32_t threshold,
+                           uint32_t seed_lo, uint32_t seed_hi) {
+  if (threshold == 0u) return false;
+  const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
+  u32x4 c = {round, lo, hi, TAG_CHN};
+  return philox4x32_10(c, seed_lo, seed_hi).x < threshold;
+}
+
+}  // namespace p2pg

@@ -1,0 +1,556 @@
+// HIP kernels (gfx950 / CDNA4) of the broadcast/relay engine.
+//
+// Data layout in HBM (one engine = one GPU):
+//   seen, F[2], next[2] : uint64 planes [V][W], row = one peer, bit (m & 63) of word (m >> 6)
+//                         = message m; W = 64 words = 512 B rows at 4096 concurrent broadcasts
+//   A[2], T[2], S       : 1 bit per peer (uint32 words); A = "first receipt this round",
+//                         T = "gossip pushes landed this round", S = "all messages seen"
+//   rowptr int64 [V+1], colidx int32 [nnz] (ascending neighbour ids per row)
+// A frontier row F[r&1][v] is only valid while A[r&1] has v's bit: rows are written whole
+// (zeros included) whenever the bit is set, so nothing is ever cleared plane-wide.
+//
+// Reference semantics (p2pnetwork): a peer that receives a broadcast for the first time
+// forwards it to every connection except the sender (Node.send_to_nodes(data,
+// exclude=[sender]), node.py:106-112, one send_to_node per target, node.py:114-120) and drops
+// later copies (app dedup, README.md:20).  Round-synchronous: all sends of round r-1 arrive in
+// round r; the parent is the lowest-id neighbour whose copy arrived first.  Relays per first
+// receipt: deg-1 (deg at the origin); gossip: min(k, deg).
+//
+// Wave model: one 64-lane wave per peer row, lane = word of the row, so every frontier/seen
+// access is one coalesced 512 B row access (measured 5.3 TB/s for random 512 B row gathers,
+// tools/microbench/atomics.hip).  Tasks = 32-peer bitmap words, grid-stride over a fixed grid
+// so stats need few atomics.
+#include <hip/hip_runtime.h>
+
+#include "internal.h"
+#include "philox.h"
+
+namespace p2pg {
+namespace {
+
+constexpr int WPB = 4;  // waves per block (256 threads)
+constexpr int GRID_MAX = 2048;
+
+__device__ __forceinline__ bool bit_test(const uint32_t* bm, int64_t v) {
+  return (bm[v >> 5] >> (v & 31)) & 1u;
+}
+
+__device__ __forceinline__ uint64_t full_mask(int w, int W, int M) {
+  if (w < W - 1 || (M & 63) == 0) return ~0ull;
+  return (1ull << (M & 63)) - 1ull;
+}
+
+__device__ __forceinline__ uint64_t wave_sum(uint64_t x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+  return x;
+}
+
+__device__ __forceinline__ void flush_stats(unsigned long long* stats, const uint64_t* c,
+                                            int lane) {
+  unsigned long long* shard = stats + (blockIdx.x & (STAT_SHARDS - 1)) * STAT_N;
+#pragma unroll
+  for (int i = 0; i < STAT_N; ++i) {
+    const uint64_t s = wave_sum(c[i]);
+    if (lane == 0 && s) atomicAdd(shard + i, (unsigned long long)s);
+  }
+}
+
+// wave index inside the block, forced into an SGPR so task indices stay scalar
+__device__ __forceinline__ int wave_in_block() {
+  return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+}
+
+// ---------------------------------------------------------------------------------------
+// Round 0: origination.  Each message m sets its bit at src[m] in F[0] and seen, and the
+// peer's A[0] bit (Node.send_to_nodes at the origin, node.py:106).
+__global__ void k_zero_rows(uint64_t* plane, int32_t W, const int32_t* rows, int32_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)n * W) return;
+  const int64_t r = rows[i / W];
+  plane[r * W + (i % W)] = 0ull;
+}
+
+__global__ void k_seed(DevState st, const int32_t* src, int32_t M) {
+  const int m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= M) return;
+  const int64_t v = src[m];
+  const uint64_t bit = 1ull << (m & 63);
+  const int64_t o = v * st.W + (m >> 6);
+  atomicOr((unsigned long long*)&st.F[0][o], (unsigned long long)bit);
+  atomicOr((unsigned long long*)&st.seen[o], (unsigned long long)bit);
+  atomicOr(&st.A[0][v >> 5], 1u << (v & 31));
+}
+
+// ---------------------------------------------------------------------------------------
+// Flood, round r >= 1, pull form: for every unsaturated peer u, OR the round-(r-1) frontier
+// rows of its active neighbours (arrivals of round r), mask with ~seen (dedup), write the new
+// frontier row.  Reads only -- no atomics on the planes (row atomics measured 4x slower than
+// row reads on MI355X).  Lanes whose word is already full skip their loads.
+template <bool CHURN>
+__global__ __launch_bounds__(256) void k_flood_pull(DevGraph g, DevState st, RoundParams p) {
+  const int lane = threadIdx.x & 63;
+  const int wib = wave_in_block();
+  const int64_t V = g.V;
+  const int W = st.W;
+  const int cur = p.round & 1, prv = cur ^ 1;
+  const uint64_t* __restrict__ Fp = st.F[prv];
+  uint64_t* __restrict__ Fc = st.F[cur];
+  const uint32_t* __restrict__ Ap = st.A[prv];
+  const int64_t ntasks = (V + 31) >> 5;
+  const int nslices = (W + 63) >> 6;
+  uint64_t c[STAT_N] = {0, 0, 0, 0, 0, 0, 0, 0};
+
+  for (int64_t task = (int64_t)blockIdx.x * WPB + wib; task < ntasks;
+       task += (int64_t)gridDim.x * WPB) {
+    const int64_t u0 = task << 5;
+    const uint32_t sat0 = st.S[task];
+    uint32_t sat = sat0;
+    uint32_t todo = ~sat0;
+    if (V - u0 < 32) todo &= (1u << (V - u0)) - 1u;
+    uint32_t aw = 0;
+    while (todo) {
+      const int b = __builtin_ctz(todo);
+      todo &= todo - 1u;
+      const int64_t u = u0 + b;
+      const int64_t beg = g.rowptr[u], end = g.rowptr[u + 1];
+      const uint64_t deg = (uint64_t)(end - beg);
+      bool row_new = false, row_full = true;
+      for (int sl = 0; sl < nslices; ++sl) {
+        const int w = sl * 64 + lane;
+        const bool valid = w < W;
+        const uint64_t fm = valid ? full_mask(w, W, st.M) : 0ull;
+        const uint64_t s = valid ? st.seen[u * W + w] : 0ull;
+        const uint64_t need = fm & ~s;
+        uint64_t acc = 0;
+        if (__ballot(need != 0ull)) {
+          for (int64_t cb = beg; cb < end; cb += 64) {
+            const int64_t j = cb + lane;
+            int32_t v = 0;
+            bool act = false;
+            if (j < end) {
+              v = g.colidx[j];
+              act = bit_test(Ap, v);
+              if (CHURN && act)
+                act = !churn_dropped((uint32_t)(p.round - 1), (uint32_t)u, (uint32_t)v,
+                                     p.churn_thr, p.cseed_lo, p.cseed_hi);
+            }
+            uint64_t m = __ballot(act);
+            while (m) {
+              int32_t vv[8];
+#pragma unroll
+              for (int k = 0; k < 8; ++k) {
+                if (m) {
+                  const int idx = __builtin_ctzll(m);
+                  m &= m - 1ull;
+                  vv[k] = __builtin_amdgcn_readlane(v, idx);
+                } else {
+                  vv[k] = -1;
+                }
+              }
+              uint64_t x[8];
+#pragma unroll
+              for (int k = 0; k < 8; ++k)
+                x[k] = (vv[k] >= 0 && need) ? Fp[(int64_t)vv[k] * W + w] : 0ull;
+#pragma unroll
+              for (int k = 0; k < 8; ++k) acc |= x[k];
+            }
+          }
+        }
+        const uint64_t nw = acc & need;
+        const bool any = __ballot(nw != 0ull) != 0ull;
+        row_new |= any;
+        if (__ballot(valid && (s | nw) != fm)) row_full = false;
+        if (nw) st.seen[u * W + w] = s | nw;
+        // single-slice rows are written only when active; multi-slice rows always (a row
+        // must be whole whenever its A bit is set)
+        if (valid && (any || nslices > 1)) Fc[u * W + w] = nw;
+        if (nw) {
+          const uint64_t pc = (uint64_t)__popcll(nw);
+          c[ST_NEW] += pc;
+          c[ST_RELAYS] += pc * (deg - 1);
+          c[ST_ACTIVE_W] += 1;
+          c[ST_WEDGES] += deg;
+        }
+      }
+      if (row_new) {
+        aw |= 1u << b;
+        if (lane == 0) {
+          c[ST_ACTIVE_V] += 1;
+          c[ST_DEG_ACT] += deg;
+        }
+      }
+      if (row_full) sat |= 1u << b;
+    }
+    if (lane == 0) {
+      st.A[cur][task] = aw;
+      if (sat != sat0) st.S[task] = sat;
+    }
+  }
+  flush_stats(st.stats, c, lane);
+}
+
+// ---------------------------------------------------------------------------------------
+// Gossip, round r >= 1, part 1: consume the pushes of round r-1 (next[r&1], touched bitmap
+// T[r&1]), dedup against seen, write the round-r frontier row and A bit, clear what was
+// consumed.  Relays: min(k, deg) per first receipt.
+__global__ __launch_bounds__(256) void k_gossip_update(DevGraph g, DevState st,
+                                                        RoundParams p) {
+  const int lane = threadIdx.x & 63;
+  const int wib = wave_in_block();
+  const int64_t V = g.V;
+  const int W = st.W;
+  const int cur = p.round & 1;
+  uint64_t* __restrict__ nx = st.next[cur];
+  uint64_t* __restrict__ Fc = st.F[cur];
+  const int64_t ntasks = (V + 31) >> 5;
+  const int nslices = (W + 63) >> 6;
+  uint64_t c[STAT_N] = {0, 0, 0, 0, 0, 0, 0, 0};
+
+  for (int64_t task = (int64_t)blockIdx.x * WPB + wib; task < ntasks;
+       task += (int64_t)gridDim.x * WPB) {
+    uint32_t tw = st.T[cur][task];
+    uint32_t aw = 0;
+    if (tw && lane == 0) st.T[cur][task] = 0u;
+    while (tw) {
+      const int b = __builtin_ctz(tw);
+      tw &= tw - 1u;
+      const int64_t u = (task << 5) + b;
+      const int64_t deg = g.rowptr[u + 1] - g.rowptr[u];
+      const uint64_t fan = (uint64_t)(deg < p.fanout ? deg : p.fanout);
+      bool row_new = false;
+      for (int sl = 0; sl < nslices; ++sl) {
+        const int w = sl * 64 + lane;
+        const bool valid = w < W;
+        uint64_t x = 0, s = 0;
+        if (valid) {
+          x = nx[u * W + w];
+          if (x) {
+            nx[u * W + w] = 0ull;
+            s = st.seen[u * W + w];
+            c[ST_AUX] += 1;  // touched (pushed-to) words consumed
+          }
+        }
+        const uint64_t nw = x & ~s;
+        const bool any = __ballot(nw != 0ull) != 0ull;
+        row_new |= any;
+        if (nw) st.seen[u * W + w] = s | nw;
+        if (valid && (any || nslices > 1)) Fc[u * W + w] = nw;
+        if (nw) {
+          const uint64_t pc = (uint64_t)__popcll(nw);
+          c[ST_NEW] += pc;
+          c[ST_RELAYS] += pc * fan;
+          c[ST_ACTIVE_W] += 1;
+          c[ST_WEDGES] += (uint64_t)deg;
+        }
+      }
+      if (row_new) {
+        aw |= 1u << b;
+        if (lane == 0) {
+          c[ST_ACTIVE_V] += 1;
+          c[ST_DEG_ACT] += (uint64_t)deg;
+        }
+      }
+    }
+    if (lane == 0) st.A[cur][task] = aw;
+  }
+  flush_stats(st.stats, c, lane);
+}
+
+// Gossip, round r >= 0, part 2: every first receipt (v, m) of round r is pushed to k
+// Philox-chosen neighbours.  One wave per (source, GCHUNK-neighbour chunk):
+// each lane (= word) builds, in its own LDS column, the per-target masks of the chunk, then
+// every nonzero target mask goes out as one coalesced 512 B row atomicOr.
+template <bool CHURN, int K>
+__global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st, RoundParams p,
+                                                        const int64_t* __restrict__ hub_items,
+                                                        int64_t n_hub) {
+  __shared__ uint64_t tbl[WPB][GCHUNK][64];
+  const int lane = threadIdx.x & 63;
+  const int wib = wave_in_block();
+  const int64_t V = g.V;
+  const int W = st.W;
+  const int cur = p.round & 1, nxt = cur ^ 1;
+  const uint64_t* __restrict__ Fc = st.F[cur];
+  uint64_t* __restrict__ nx = st.next[nxt];
+  uint32_t* __restrict__ Tn = st.T[nxt];
+  const int64_t nwords = (V + 31) >> 5;
+  const int64_t ntasks = nwords + n_hub;
+  const int nslices = (W + 63) >> 6;
+  const int k = K > 0 ? K : p.fanout;
+  uint64_t c[STAT_N] = {0, 0, 0, 0, 0, 0, 0, 0};
+
+  for (int64_t task = (int64_t)blockIdx.x * WPB + wib; task < ntasks;
+       task += (int64_t)gridDim.x * WPB) {
+    uint32_t todo;
+    int64_t base;
+    int chunk;
+    if (task < nwords) {
+      todo = st.A[cur][task];
+      base = task << 5;
+      chunk = 0;
+    } else {
+      const int64_t it = hub_items[task - nwords];
+      base = it >> 32;
+      chunk = (int)(it & 0xFFFFFFFFll);
+      todo = bit_test(st.A[cur], base) ? 1u : 0u;
+    }
+    while (todo) {
+      const int b = __builtin_ctz(todo);
+      todo &= todo - 1u;
+      const int64_t v = task < nwords ? base + b : base;
+      const int64_t rb = g.rowptr[v];
+      const int64_t deg = g.rowptr[v + 1] - rb;
+      if (task < nwords && deg > GCHUNK) continue;  // hub: handled by its chunk items
+      const int nb = chunk * GCHUNK;
+      const int nn = (int)(deg - nb < GCHUNK ? deg - nb : GCHUNK);
+      const bool all = deg <= k;
+      for (int sl = 0; sl < nslices; ++sl) {
+        const int w = sl * 64 + lane;
+        const uint64_t f = w < W ? Fc[v * W + w] : 0ull;
+        if (!__ballot(f != 0ull)) continue;
+        if (!all) {
+          for (int j = 0; j < nn; ++j) tbl[wib][j][lane] = 0ull;
+          uint64_t rem = f;
+          while (rem) {
+            const int bit = __builtin_ctzll(rem);
+            rem &= rem - 1ull;
+            const uint32_t mg = p.msg_base + (uint32_t)(w * 64 + bit);
+            if constexpr (K > 0) {
+              uint32_t pk[K];
+              gossip_picks_t<K>((uint32_t)p.round, (uint32_t)v, mg, (uint32_t)deg, p.gseed_lo,
+                                p.gseed_hi, pk);
+#pragma unroll
+              for (int q = 0; q < K; ++q) {
+                const uint32_t jj = pk[q] - (uint32_t)nb;
+                if (jj < (uint32_t)nn) tbl[wib][jj][lane] |= 1ull << bit;
+              }
+            } else {
+              uint32_t pk[16];
+              gossip_picks((uint32_t)p.round, (uint32_t)v, mg, (uint32_t)deg, k, p.gseed_lo,
+                           p.gseed_hi, pk);
+              for (int q = 0; q < k; ++q) {
+                const uint32_t jj = pk[q] - (uint32_t)nb;
+                if (jj < (uint32_t)nn) tbl[wib][jj][lane] |= 1ull << bit;
+              }
+            }
+          }
+        }
+        for (int j = 0; j < nn; ++j) {
+          const uint64_t x = all ? f : tbl[wib][j][lane];
+          const uint64_t bal = __ballot(x != 0ull);
+          if (!bal) continue;
+          const int32_t u = g.colidx[rb + nb + j];
+          if (CHURN && churn_dropped((uint32_t)p.round, (uint32_t)v, (uint32_t)u, p.churn_thr,
+                                     p.cseed_lo, p.cseed_hi))
+            continue;
+          if (x) atomicOr((unsigned long long*)&nx[(int64_t)u * W + w], (unsigned long long)x);
+          if (lane == 0) {
+            atomicOr(&Tn[u >> 5], 1u << (u & 31));
+            c[ST_SCATTER] += (uint64_t)__popcll(bal);
+          }
+        }
+      }
+    }
+  }
+  flush_stats(st.stats, c, lane);
+}
+
+// ---------------------------------------------------------------------------------------
+// Validation: the lowest-id neighbour v whose round-(r-1) send of message m reached u
+// (receivers process senders in ascending id -- the harness's stand-in for TCP arrival
+// order).  Returns -2 if none (cannot happen for a first receipt at r >= 1).
+__device__ int32_t find_parent(const DevGraph& g, const DevState& st, const RoundParams& p,
+                               int64_t u, int m) {
+  const int prv = (p.round & 1) ^ 1;
+  const int W = st.W;
+  const uint64_t bit = 1ull << (m & 63);
+  const int w = m >> 6;
+  const int64_t beg = g.rowptr[u], end = g.rowptr[u + 1];
+  for (int64_t e = beg; e < end; ++e) {
+    const int32_t v = g.colidx[e];
+    if (!bit_test(st.A[prv], v)) continue;
+    if (!(st.F[prv][(int64_t)v * W + w] & bit)) continue;
+    if (p.churn_thr && churn_dropped((uint32_t)(p.round - 1), (uint32_t)u, (uint32_t)v,
+                                     p.churn_thr, p.cseed_lo, p.cseed_hi))
+      continue;
+    if (p.mode == 1) {
+      const int64_t vb = g.rowptr[v];
+      const int64_t dv = g.rowptr[v + 1] - vb;
+      if (dv > p.fanout) {
+        int64_t lo = 0, hi = dv;  // position of u in v's ascending list
+        while (lo < hi) {
+          const int64_t mid = (lo + hi) >> 1;
+          if (g.colidx[vb + mid] < u) lo = mid + 1; else hi = mid;
+        }
+        uint32_t pk[16];
+        gossip_picks((uint32_t)(p.round - 1), (uint32_t)v, p.msg_base + (uint32_t)m,
+                     (uint32_t)dv, p.fanout, p.gseed_lo, p.gseed_hi, pk);
+        bool hit = false;
+        for (int q = 0; q < p.fanout; ++q) hit |= (pk[q] == (uint32_t)lo);
+        if (!hit) continue;
+      }
+    }
+    return v;
+  }
+  return -2;
+}
+
+__global__ __launch_bounds__(256) void k_record(DevGraph g, DevState st, RoundParams p) {
+  const int lane = threadIdx.x & 63;
+  const int wib = wave_in_block();
+  const int cur = p.round & 1;
+  const int W = st.W;
+  const int64_t ntasks = (g.V + 31) >> 5;
+  const int nslices = (W + 63) >> 6;
+  for (int64_t task = (int64_t)blockIdx.x * WPB + wib; task < ntasks;
+       task += (int64_t)gridDim.x * WPB) {
+    uint32_t aw = st.A[cur][task];
+    while (aw) {
+      const int b = __builtin_ctz(aw);
+      aw &= aw - 1u;
+      const int64_t u = (task << 5) + b;
+      for (int sl = 0; sl < nslices; ++sl) {
+        const int w = sl * 64 + lane;
+        uint64_t f = w < W ? st.F[cur][u * W + w] : 0ull;
+        while (f) {
+          const int bit = __builtin_ctzll(f);
+          f &= f - 1ull;
+          const int m = w * 64 + bit;
+          st.hop[u * st.M + m] = p.round;
+          st.parent[u * st.M + m] = p.round == 0 ? -1 : find_parent(g, st, p, u, m);
+        }
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_deliveries(DevGraph g, DevState st, RoundParams p,
+                                                    int64_t cap, int32_t* peer, int32_t* msg,
+                                                    int32_t* parent,
+                                                    unsigned long long* counter) {
+  const int lane = threadIdx.x & 63;
+  const int wib = wave_in_block();
+  const int cur = p.round & 1;
+  const int W = st.W;
+  const int64_t ntasks = (g.V + 31) >> 5;
+  const int nslices = (W + 63) >> 6;
+  for (int64_t task = (int64_t)blockIdx.x * WPB + wib; task < ntasks;
+       task += (int64_t)gridDim.x * WPB) {
+    uint32_t aw = st.A[cur][task];
+    while (aw) {
+      const int b = __builtin_ctz(aw);
+      aw &= aw - 1u;
+      const int64_t u = (task << 5) + b;
+      for (int sl = 0; sl < nslices; ++sl) {
+        const int w = sl * 64 + lane;
+        uint64_t f = w < W ? st.F[cur][u * W + w] : 0ull;
+        while (f) {
+          const int bit = __builtin_ctzll(f);
+          f &= f - 1ull;
+          const int m = w * 64 + bit;
+          const unsigned long long pos = atomicAdd(counter, 1ull);
+          if ((int64_t)pos < cap) {
+            peer[pos] = (int32_t)u;
+            msg[pos] = m;
+            parent[pos] = p.round == 0 ? -1 : find_parent(g, st, p, u, m);
+          }
+        }
+      }
+    }
+  }
+}
+
+__global__ void k_philox(int32_t n, const uint32_t* ctr, uint32_t k0, uint32_t k1,
+                         uint32_t* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  u32x4 c = {ctr[4 * i], ctr[4 * i + 1], ctr[4 * i + 2], ctr[4 * i + 3]};
+  u32x4 r = philox4x32_10(c, k0, k1);
+  out[4 * i] = r.x;
+  out[4 * i + 1] = r.y;
+  out[4 * i + 2] = r.z;
+  out[4 * i + 3] = r.w;
+}
+
+int grid_tasks(int64_t ntasks) {
+  int64_t b = (ntasks + WPB - 1) / WPB;
+  return (int)(b < 1 ? 1 : (b > GRID_MAX ? GRID_MAX : b));
+}
+
+}  // namespace
+
+hipError_t launch_zero_rows(uint64_t* plane, int32_t W, const int32_t* rows, int32_t n,
+                            hipStream_t s) {
+  const int64_t tot = (int64_t)n * W;
+  if (tot == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_zero_rows, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, plane,
+                     W, rows, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_seed(const DevState& st, const int32_t* src, int32_t M, hipStream_t s) {
+  if (M == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_seed, dim3((M + 255) / 256), dim3(256), 0, s, st, src, M);
+  return hipGetLastError();
+}
+
+hipError_t launch_flood_pull(const DevGraph& g, const DevState& st, const RoundParams& p,
+                             hipStream_t s) {
+  const int grid = grid_tasks((g.V + 31) >> 5);
+  if (p.churn_thr)
+    hipLaunchKernelGGL(k_flood_pull<true>, dim3(grid), dim3(256), 0, s, g, st, p);
+  else
+    hipLaunchKernelGGL(k_flood_pull<false>, dim3(grid), dim3(256), 0, s, g, st, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_gossip_update(const DevGraph& g, const DevState& st, const RoundParams& p,
+                                hipStream_t s) {
+  const int grid = grid_tasks((g.V + 31) >> 5);
+  hipLaunchKernelGGL(k_gossip_update, dim3(grid), dim3(256), 0, s, g, st, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_gossip_scatter(const DevGraph& g, const DevState& st, const RoundParams& p,
+                                 const int64_t* hub_items, int64_t n_hub_items, hipStream_t s) {
+  const int grid = grid_tasks(((g.V + 31) >> 5) + n_hub_items);
+#define P2PG_SCATTER(CH, KK)                                                                 \
+  hipLaunchKernelGGL((k_gossip_scatter<CH, KK>), dim3(grid), dim3(256), 0, s, g, st, p,      \
+                     hub_items, n_hub_items)
+  const bool ch = p.churn_thr != 0;
+  switch (p.fanout) {
+    case 1: if (ch) P2PG_SCATTER(true, 1); else P2PG_SCATTER(false, 1); break;
+    case 2: if (ch) P2PG_SCATTER(true, 2); else P2PG_SCATTER(false, 2); break;
+    case 3: if (ch) P2PG_SCATTER(true, 3); else P2PG_SCATTER(false, 3); break;
+    case 4: if (ch) P2PG_SCATTER(true, 4); else P2PG_SCATTER(false, 4); break;
+    default: if (ch) P2PG_SCATTER(true, 0); else P2PG_SCATTER(false, 0); break;
+  }
+#undef P2PG_SCATTER
+  return hipGetLastError();
+}
+
+hipError_t launch_record(const DevGraph& g, const DevState& st, const RoundParams& p,
+                         hipStream_t s) {
+  const int grid = grid_tasks((g.V + 31) >> 5);
+  hipLaunchKernelGGL(k_record, dim3(grid), dim3(256), 0, s, g, st, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_deliveries(const DevGraph& g, const DevState& st, const RoundParams& p,
+                             int64_t cap, int32_t* peer, int32_t* msg, int32_t* parent,
+                             unsigned long long* counter, hipStream_t s) {
+  const int grid = grid_tasks((g.V + 31) >> 5);
+  hipLaunchKernelGGL(k_deliveries, dim3(grid), dim3(256), 0, s, g, st, p, cap, peer, msg,
+                     parent, counter);
+  return hipGetLastError();
+}
+
+hipError_t launch_philox(int32_t n, const uint32_t* ctr, uint32_t k0, uint32_t k1,
+                         uint32_t* out, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_philox, dim3((n + 255) / 256), dim3(256), 0, s, n, ctr, k0, k1, out);
+  return hipGetLastError();
+}
+
+}  // namespace p2pg

@@ -1,0 +1,253 @@
+"""GraphNetwork: a whole population of relaying p2pnetwork peers on one MI355X.
+
+What an application builds on p2pnetwork for a broadcast is (pj8912/python-p2p-network):
+
+    class MyNode(Node):                                   # p2pnetwork/node.py:13
+        def node_message(self, node, data):               # node.py:334-338
+            if data["id"] in self.seen: return            # dedup, README.md:20
+            self.seen.add(data["id"])
+            self.send_to_nodes(data, exclude=[node])      # node.py:106-112 -> send_to_node
+                                                          #   (message_count_send += 1, :116)
+
+GraphNetwork runs that relay for every peer of a ``PeerGraph`` at once, for up to thousands of
+concurrent broadcasts (64 per uint64 word), round-synchronously, through the HIP engine behind
+the C-ABI of include/p2pgpu.h.  The hook surface is kept in batched form: per round,
+``node_message_batch(deliveries)`` receives the first receipts of that round as arrays
+(peer, msg, hop, parent) -- the node_message events that pass dedup -- and a
+``callback(event, network, connected_node, data)`` with the reference signature
+(node.py:25-29) is invoked with event "node_message_batch".  Per-callback replay for Node
+subclasses is in ``p2pnetwork.gpu.compat``.
+"""
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from .graph import PeerGraph
+
+STAT_FIELDS = ("round", "active", "new_deliveries", "relays", "active_vertices", "active_words",
+               "wedges", "deg_active", "scatter_words", "touched_words")
+
+
+@dataclass
+class RoundStats:
+    round: int
+    active: int
+    new_deliveries: int
+    relays: int
+    active_vertices: int
+    active_words: int
+    wedges: int
+    deg_active: int
+    scatter_words: int
+    touched_words: int
+
+    @classmethod
+    def from_c(cls, s):
+        return cls(*(int(getattr(s, f)) for f in STAT_FIELDS))
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f in STAT_FIELDS}
+
+
+@dataclass
+class Deliveries:
+    """First receipts of one round, sorted by (peer, msg); parent = -1 at the origin."""
+    peer: np.ndarray
+    msg: np.ndarray
+    hop: np.ndarray
+    parent: np.ndarray
+
+    def __len__(self):
+        return len(self.peer)
+
+
+def churn_threshold(p_drop):
+    """floor(p_drop * 2^32), the integer threshold of the per-round edge-drop mask."""
+    if not 0.0 <= p_drop < 1.0:
+        raise ValueError("churn probability must be in [0, 1)")
+    return int(np.floor(p_drop * 4294967296.0))
+
+
+class GraphNetwork:
+    """A peer graph resident in HBM plus the relay engine that floods/gossips over it."""
+
+    def __init__(self, graph, mode="flood", fanout=3, gossip_seed=0x5EED, churn=0.0,
+                 churn_threshold_value=None, churn_seed=0xC0FFEE, record=False, timing=False,
+                 device=0, msg_id_base=0, callback=None):
+        if not isinstance(graph, PeerGraph):
+            raise TypeError("graph must be a PeerGraph")
+        if mode not in ("flood", "gossip"):
+            raise ValueError("mode must be 'flood' or 'gossip'")
+        self.graph = graph
+        self.mode = mode
+        self.fanout = int(fanout)
+        self.record = bool(record)
+        self.callback = callback
+        cfg = _lib.Config()
+        cfg.mode = _lib.MODE_FLOOD if mode == "flood" else _lib.MODE_GOSSIP
+        cfg.fanout = self.fanout
+        cfg.gossip_seed = int(gossip_seed)
+        cfg.churn_seed = int(churn_seed)
+        cfg.churn_threshold = int(churn_threshold_value if churn_threshold_value is not None
+                                  else churn_threshold(churn))
+        cfg.msg_id_base = int(msg_id_base)
+        cfg.flags = (_lib.FLAG_RECORD if record else 0) | (_lib.FLAG_TIMING if timing else 0)
+        cfg.device = int(device)
+        self.config = cfg
+        L = _lib.lib()
+        h = ctypes.c_void_p()
+        _lib.check(L.p2pg_create(ctypes.byref(cfg), ctypes.byref(h)))
+        self._h = h
+        self._check(L.p2pg_load_csr(h, graph.V, _lib.ptr(graph.rowptr), _lib.ptr(graph.colidx)))
+        self.sources = None
+        self.rounds = []
+        self.message_count_send = 0  # sum of Node.message_count_send (node.py:65, :116)
+
+    # -- plumbing -------------------------------------------------------------------------
+    def _check(self, rc):
+        return _lib.check(rc, self._h)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.lib().p2pg_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def M(self):
+        return 0 if self.sources is None else len(self.sources)
+
+    @property
+    def W(self):
+        return (self.M + 63) // 64
+
+    def set_stream(self, hip_stream):
+        """Launch on an external hipStream_t handle (int), e.g. torch's current stream."""
+        self._check(_lib.lib().p2pg_set_stream(self._h, ctypes.c_void_p(hip_stream or None)))
+
+    # -- broadcasts -----------------------------------------------------------------------
+    def broadcast(self, sources):
+        """Originate one broadcast per entry (origin peer ids); message m = position m.
+        Equivalent of calling Node.send_to_nodes(data) at each origin (node.py:106)."""
+        src = np.ascontiguousarray(sources, dtype=np.int32)
+        if src.ndim != 1 or len(src) == 0:
+            raise ValueError("sources must be a non-empty 1-D array of peer ids")
+        self._check(_lib.lib().p2pg_set_sources(self._h, len(src), _lib.ptr(src)))
+        self.sources = src
+        self.rounds = []
+        self.message_count_send = 0
+
+    def reset(self):
+        self._check(_lib.lib().p2pg_reset(self._h))
+        self.rounds = []
+        self.message_count_send = 0
+
+    def step(self):
+        """Run one round; returns its RoundStats (``active`` = messages still in flight)."""
+        s = _lib.RoundStatsC()
+        self._check(_lib.lib().p2pg_step(self._h, ctypes.byref(s)))
+        st = RoundStats.from_c(s)
+        self.rounds.append(st)
+        self.message_count_send += st.relays
+        if st.new_deliveries and self._wants_deliveries():
+            self.node_message_batch(self.deliveries())
+        return st
+
+    def run(self, max_rounds=1 << 20):
+        """Rounds until quiescence; returns the list of RoundStats (last one has no receipts)."""
+        if not self._wants_deliveries():
+            buf = (_lib.RoundStatsC * max(1, min(max_rounds, 4096)))()
+            out = []
+            while len(out) < max_rounds:
+                n = ctypes.c_int32()
+                chunk = min(max_rounds - len(out), len(buf))
+                rc = self._check(_lib.lib().p2pg_run(self._h, chunk, buf, ctypes.byref(n)))
+                for i in range(n.value):
+                    st = RoundStats.from_c(buf[i])
+                    out.append(st)
+                    self.rounds.append(st)
+                    self.message_count_send += st.relays
+                if rc == 0 or n.value == 0:
+                    break
+            return out
+        out = []
+        while len(out) < max_rounds:
+            st = self.step()
+            out.append(st)
+            if not st.active:
+                break
+        return out
+
+    # -- the batched hook (override like Node.node_message, node.py:334-338) --------------
+    def node_message_batch(self, deliveries):
+        if self.callback is not None:
+            self.callback("node_message_batch", self, None, deliveries)
+
+    def _wants_deliveries(self):
+        return (self.callback is not None
+                or type(self).node_message_batch is not GraphNetwork.node_message_batch)
+
+    def deliveries(self, cap=None):
+        """First receipts of the most recent round as (peer, msg, hop, parent) arrays."""
+        if cap is None:
+            cap = self.rounds[-1].new_deliveries if self.rounds else 0
+        cap = int(cap)
+        peer = np.zeros(max(cap, 1), dtype=np.int32)
+        msg = np.zeros_like(peer)
+        hop = np.zeros_like(peer)
+        parent = np.zeros_like(peer)
+        n = ctypes.c_int64()
+        self._check(_lib.lib().p2pg_get_new_deliveries(
+            self._h, cap, _lib.ptr(peer), _lib.ptr(msg), _lib.ptr(hop), _lib.ptr(parent), ctypes.byref(n)))
+        k = min(n.value, cap)
+        return Deliveries(peer[:k], msg[:k], hop[:k], parent[:k])
+
+    # -- validation planes ----------------------------------------------------------------
+    def seen_plane(self):
+        out = np.zeros((self.graph.V, self.W), dtype=np.uint64)
+        self._check(_lib.lib().p2pg_read_planes(self._h, _lib.ptr(out), None, None))
+        return out
+
+    def delivered(self):
+        """bool [V, M]: peer v has received broadcast m (its dedup 'seen' set)."""
+        s = self.seen_plane()
+        bits = np.unpackbits(s.view(np.uint8).reshape(self.graph.V, -1), axis=1, bitorder="little")
+        return bits[:, :self.M].astype(bool)
+
+    def hop_parent(self):
+        """(hop, parent) int32 [V, M]; needs record=True.  -1 = not delivered / origin."""
+        if not self.record:
+            raise RuntimeError("hop/parent planes need GraphNetwork(record=True)")
+        hop = np.zeros((self.graph.V, self.M), dtype=np.int32)
+        par = np.zeros_like(hop)
+        self._check(_lib.lib().p2pg_read_planes(self._h, None, _lib.ptr(hop), _lib.ptr(par)))
+        return hop, par
+
+    def kernel_times(self):
+        """Summed device ms and launch counts per kernel class (needs timing=True)."""
+        ms = np.zeros(4, dtype=np.float64)
+        n = np.zeros(4, dtype=np.int64)
+        self._check(_lib.lib().p2pg_kernel_times(self._h, _lib.ptr(ms), _lib.ptr(n)))
+        names = ("seed_update", "flood_pull", "gossip_scatter", "record")
+        return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(names)}
+
+    def device_philox(self, ctr, key):
+        """Evaluate Philox4x32-10 on the GPU for counters [n, 4] (KAT hook)."""
+        c = np.ascontiguousarray(ctr, dtype=np.uint32).reshape(-1, 4)
+        k = np.ascontiguousarray(key, dtype=np.uint32)
+        out = np.zeros_like(c)
+        self._check(_lib.lib().p2pg_device_philox(self._h, len(c), _lib.ptr(c), _lib.ptr(k), _lib.ptr(out)))
+        return out

@@ -1,0 +1,249 @@
+"""GPU parity: the HIP engine (through the C-ABI) against the golden fixtures produced with the
+reference's own Node objects and against the CPU oracle -- bit-exact hop, parent, delivered
+set, per-round relays and byte-model counters; plus size-independent properties at the
+BASELINE.json full sizes (config 3 flood, config 4 gossip)."""
+import zlib
+
+import numpy as np
+import pytest
+
+from conftest import golden_cases, load_golden, trim_zeros
+from oracle import philox, relay_oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def gpu_net(z_or_graph, mode="flood", fanout=3, gseed=0, thr=0, cseed=0, record=True, **kw):
+    from p2pnetwork.gpu import GraphNetwork, PeerGraph
+    g = z_or_graph if isinstance(z_or_graph, PeerGraph) else PeerGraph(z_or_graph["rowptr"], z_or_graph["colidx"])
+    return GraphNetwork(g, mode=mode, fanout=fanout, gossip_seed=gseed, churn_threshold_value=thr,
+                        churn_seed=cseed, record=record, **kw)
+
+
+def oracle_for(rowptr, colidx, src, mode, fanout, gseed, thr, cseed):
+    if mode == "flood":
+        return relay_oracle.flood(rowptr, colidx, src, thr, cseed)
+    return relay_oracle.gossip(rowptr, colidx, src, fanout, gseed, 0, thr, cseed)
+
+
+STAT_KEYS = ("new_deliveries", "relays", "active_vertices", "active_words", "wedges", "deg_active",
+             "scatter_words")
+
+
+def assert_rounds_equal(gpu_rounds, ora_rounds):
+    g = [r.as_dict() for r in gpu_rounds]
+    o = list(ora_rounds)
+    n = max(len(g), len(o))
+    blank = {k: 0 for k in STAT_KEYS}
+    for i in range(n):
+        a = g[i] if i < len(g) else blank
+        b = o[i] if i < len(o) else blank
+        for k in STAT_KEYS:
+            assert a[k] == b[k], (i, k, a[k], b[k])
+
+
+@pytest.mark.parametrize("name", golden_cases())
+def test_gpu_matches_reference_golden(name):
+    z = load_golden(name)
+    mode = str(z["mode"])
+    net = gpu_net(z, mode, int(z["fanout"]), int(z["gossip_seed"]), int(z["churn_threshold"]),
+                  int(z["churn_seed"]))
+    with net:
+        net.broadcast(z["src"])
+        rounds = net.run()
+        hop, parent = net.hop_parent()
+        np.testing.assert_array_equal(hop, z["hop"])
+        np.testing.assert_array_equal(parent, z["parent"])
+        np.testing.assert_array_equal(net.delivered(), z["hop"] >= 0)
+        np.testing.assert_array_equal(trim_zeros([r.relays for r in rounds]), trim_zeros(z["round_relays"]))
+        assert net.message_count_send == int(z["round_relays"].sum())
+    ora = oracle_for(z["rowptr"], z["colidx"], z["src"], mode, int(z["fanout"]), int(z["gossip_seed"]),
+                     int(z["churn_threshold"]), int(z["churn_seed"]))
+    assert_rounds_equal(rounds, ora.rounds)
+
+
+def test_device_philox_kat():
+    from p2pnetwork.gpu import PeerGraph
+    with gpu_net(PeerGraph.ring_chords(10, 3), record=False) as net:
+        ctr = np.array([[0, 0, 0, 0], [0xFFFFFFFF] * 4, [0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344]],
+                       dtype=np.uint32)
+        out0 = net.device_philox(ctr[:1], [0, 0])
+        assert [int(x) for x in out0[0]] == [0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8]
+        out1 = net.device_philox(ctr[1:2], [0xFFFFFFFF, 0xFFFFFFFF])
+        assert [int(x) for x in out1[0]] == [0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD]
+        out2 = net.device_philox(ctr[2:3], [0xA4093822, 0x299F31D0])
+        assert [int(x) for x in out2[0]] == [0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1]
+        rng = np.random.default_rng(1)
+        c = rng.integers(0, 2**32, size=(1000, 4), dtype=np.uint64).astype(np.uint32)
+        d = net.device_philox(c, [123, 456])
+        h = np.stack(philox.philox4x32_10(*c.T.astype(np.uint64), 123, 456), axis=1)
+        np.testing.assert_array_equal(d.astype(np.uint64), h)
+
+
+CASES = [
+    ("rrg", dict(V=400, d=5), "flood", 1, 0),
+    ("rrg", dict(V=400, d=5), "flood", 63, 0),
+    ("gnp", dict(V=700, k=6.0), "flood", 65, 0),
+    ("gnp", dict(V=300, k=3.0), "flood", 130, 0),         # sparse: several components
+    ("ba", dict(V=600, m=3), "flood", 64, 0),
+    ("ba", dict(V=600, m=3), "gossip", 64, 0),
+    ("ws", dict(V=500, k=6, b=0.2), "gossip", 200, 0),
+    ("ws", dict(V=500, k=6, b=0.2), "flood", 96, 400_000_000),
+    ("ba", dict(V=400, m=5), "gossip", 64, 900_000_000),
+    ("gnp", dict(V=200, k=8.0), "flood", 4160, 0),         # W = 65: multi-slice rows
+    ("ba", dict(V=150, m=20), "gossip", 4160, 0),          # hubs > 1 chunk, W = 65
+]
+
+
+def make_graph(kind, p, seed):
+    from p2pnetwork.gpu import PeerGraph
+    if kind == "rrg":
+        return PeerGraph.random_regular(p["V"], p["d"], seed)
+    if kind == "gnp":
+        return PeerGraph.gnp(p["V"], p["k"], seed)
+    if kind == "ba":
+        return PeerGraph.barabasi_albert(p["V"], p["m"], seed)
+    return PeerGraph.watts_strogatz(p["V"], p["k"], p["b"], seed)
+
+
+@pytest.mark.parametrize("kind,p,mode,M,thr", CASES)
+@pytest.mark.parametrize("fanout", [3, 5])
+def test_gpu_matches_oracle_random(kind, p, mode, M, thr, fanout):
+    if mode == "flood" and fanout != 3:
+        pytest.skip("fanout only matters for gossip")
+    from p2pnetwork.gpu import make_sources
+    seed = zlib.crc32(repr((kind, mode, M, thr, fanout)).encode()) & 0xFFFF
+    g = make_graph(kind, p, seed)
+    src = make_sources(g.V, M, seed=seed + 1)
+    gseed, cseed = 0x1234 + seed, 0x777 + seed
+    with gpu_net(g, mode, fanout, gseed, thr, cseed) as net:
+        net.broadcast(src)
+        rounds = net.run()
+        hop, parent = net.hop_parent()
+    ora = oracle_for(g.rowptr, g.colidx, src, mode, fanout, gseed, thr, cseed)
+    np.testing.assert_array_equal(hop, ora.hop)
+    np.testing.assert_array_equal(parent, ora.parent)
+    assert_rounds_equal(rounds, ora.rounds)
+
+
+def test_deliveries_stream_and_batched_hook():
+    """The batched hook gets, per round, exactly the first receipts (peer, msg, hop, parent)
+    sorted by (peer, msg) -- the node_message events that pass dedup."""
+    from p2pnetwork.gpu import GraphNetwork, PeerGraph
+    z = load_golden("ba1000_gossip_k3")
+    got = []
+
+    class Hooked(GraphNetwork):
+        def node_message_batch(self, d):
+            got.append((d.peer.copy(), d.msg.copy(), d.hop.copy(), d.parent.copy()))
+
+    net = Hooked(PeerGraph(z["rowptr"], z["colidx"]), mode="gossip", fanout=3, gossip_seed=int(z["gossip_seed"]))
+    with net:
+        net.broadcast(z["src"])
+        net.run()
+    hop, par = z["hop"], z["parent"]
+    assert len(got) == int(hop.max()) + 1  # round 0 (origination) included
+    for r, (peer, msg, h, p) in enumerate(got):
+        vs, ms = np.nonzero(hop == r)  # row-major = sorted by (peer, msg)
+        np.testing.assert_array_equal(peer, vs)
+        np.testing.assert_array_equal(msg, ms)
+        assert (h == r).all()
+        np.testing.assert_array_equal(p, par[vs, ms])
+
+
+def test_reset_rerun_is_bitwise_deterministic():
+    from p2pnetwork.gpu import PeerGraph, make_sources
+    g = PeerGraph.barabasi_albert(20000, 4, seed=3)
+    src = make_sources(g.V, 4096, seed=9)
+    with gpu_net(g, "gossip", 3, 42, 100_000_000, 7, record=False) as net:
+        net.broadcast(src)
+        a = [r.as_dict() for r in net.run()]
+        sa = net.seen_plane()
+        net.reset()
+        b = [r.as_dict() for r in net.run()]
+        sb = net.seen_plane()
+    assert a == b
+    np.testing.assert_array_equal(sa, sb)
+
+
+def _components(g):
+    import scipy.sparse as sp
+    from scipy.sparse.csgraph import connected_components
+    A = sp.csr_matrix((np.ones(g.nnz, dtype=np.int8), g.colidx, g.rowptr), shape=(g.V, g.V))
+    return A, connected_components(A, directed=False)[1]
+
+
+def test_config3_flood_full_size_properties():
+    """Config 3 (1M-peer G(n,p) mean degree 16, 4096 floods): delivered set = connected
+    component of the origin, relays = sum_m [sum_{v in comp} deg(v) - (|comp| - 1)], first-
+    receipt rounds = BFS distances (sampled messages)."""
+    from scipy.sparse.csgraph import shortest_path
+    from p2pnetwork.gpu import PeerGraph, make_sources
+    g = PeerGraph.gnp(1_000_000, 16, seed=1)
+    M = 4096
+    src = make_sources(g.V, M, seed=1)
+    with gpu_net(g, "flood", record=False) as net:
+        net.broadcast(src)
+        rounds = net.run()
+        seen = net.seen_plane()
+    A, comp = _components(g)
+    deg = g.degree()
+    csize = np.bincount(comp)
+    cdeg = np.bincount(comp, weights=deg).astype(np.int64)
+    want_relays = int(sum(cdeg[comp[s]] - (csize[comp[s]] - 1) for s in src))
+    assert sum(r.relays for r in rounds) == want_relays
+    assert sum(r.new_deliveries for r in rounds) == int(csize[comp[src]].sum())
+    popc = np.unpackbits(seen.view(np.uint8), axis=1).sum(axis=1)
+    # every peer's seen set = messages whose origin is in its component
+    per_comp = np.bincount(comp[src], minlength=len(csize))
+    np.testing.assert_array_equal(popc, per_comp[comp])
+    # broadcasts are independent bit lanes: re-run 4 sampled origins with full recording and
+    # check first-receipt round = BFS distance and parent = lowest-id neighbour one hop closer
+    rng = np.random.default_rng(0)
+    sample = rng.choice(M, 4, replace=False)
+    d = shortest_path(A, unweighted=True, indices=src[sample])
+    with gpu_net(g, "flood", record=True) as net:
+        net.broadcast(src[sample])
+        sub = net.run()
+        hop, parent = net.hop_parent()
+    rows = np.repeat(np.arange(g.V), deg)
+    for i in range(len(sample)):
+        di = np.where(np.isfinite(d[i]), d[i], -1).astype(np.int64)
+        np.testing.assert_array_equal(hop[:, i], di)
+        best = np.full(g.V, np.iinfo(np.int64).max)
+        ok = (di[g.colidx] >= 0) & (di[g.colidx] == di[rows] - 1)
+        np.minimum.at(best, rows[ok], g.colidx[ok].astype(np.int64))
+        want = np.where(di > 0, best, -1)
+        np.testing.assert_array_equal(parent[:, i], want)
+    assert sum(r.new_deliveries for r in sub) == int((hop >= 0).sum())
+
+
+def test_config4_gossip_full_size_parity():
+    """Config 4 (10M-peer Barabasi-Albert m=4, 4096 push-gossips, k=3) at full size.
+    Broadcasts are independent bit lanes, so the first 64 of the 4096 must come out exactly as
+    a 64-broadcast run: (a) the GPU 4096 run's word-0 seen bits == the GPU 64 run's delivered
+    set; (b) the GPU 64 run's hop and parent planes == the C oracle's, bit for bit; plus every
+    first receipt relays exactly 3 (min degree 4 > k) and a reset re-run is identical."""
+    from oracle import coracle
+    from p2pnetwork.gpu import PeerGraph, make_sources
+    g = PeerGraph.barabasi_albert(10_000_000, 4, seed=1)
+    src = make_sources(g.V, 4096, seed=1)
+    with gpu_net(g, "gossip", 3, 0x5EED, record=False) as net:
+        net.broadcast(src)
+        a = net.run()
+        word0 = net.seen_plane()[:, 0].copy()
+        net.reset()
+        b = net.run()
+    assert [r.as_dict() for r in a] == [r.as_dict() for r in b]
+    for r in a:
+        assert r.relays == 3 * r.new_deliveries
+    with gpu_net(g, "gossip", 3, 0x5EED, record=True) as net:
+        net.broadcast(src[:64])
+        sub = net.run()
+        hop, parent = net.hop_parent()
+    bits = np.unpackbits(word0.view(np.uint8).reshape(g.V, 8), axis=1, bitorder="little").astype(bool)
+    np.testing.assert_array_equal(bits, hop >= 0)
+    ora = coracle.run(g.rowptr, g.colidx, src[:64], "gossip", 3, 0x5EED, record=True)
+    np.testing.assert_array_equal(hop, ora.hop)
+    np.testing.assert_array_equal(parent, ora.parent)
+    assert_rounds_equal(sub, ora.rounds)
