@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <string>
@@ -36,6 +37,10 @@ struct p2pg_engine {
   int32_t* d_colidx = nullptr;
   int64_t* d_hub = nullptr;
   int64_t n_hub = 0;
+  uint32_t* d_rev = nullptr;   // gossip: reverse edge slots
+  bool last_push_e = false;    // gossip: pushes of the previous round went to E (dense)
+  double e_thresh = 0.1;       // store-mode when active words >= thresh * active rows * W
+  int push_mode = 0;           // 0 auto, 1 always row atomics, 2 always edge stores
   int32_t* d_src = nullptr;
   DevState st{};
   size_t plane_bytes = 0, bm_bytes = 0;
@@ -87,6 +92,7 @@ void free_state(p2pg_engine* e) {
   dfree(s.S);
   dfree(s.hop);
   dfree(s.parent);
+  dfree(s.E);
   dfree(s.stats);
   dfree(e->d_src);
   e->have_state = false;
@@ -96,6 +102,7 @@ void free_graph(p2pg_engine* e) {
   dfree(e->d_rowptr);
   dfree(e->d_colidx);
   dfree(e->d_hub);
+  dfree(e->d_rev);
   e->n_hub = 0;
 }
 
@@ -113,7 +120,9 @@ RoundParams params(const p2pg_engine* e) {
   return p;
 }
 
-DevGraph graph(const p2pg_engine* e) { return DevGraph{e->d_rowptr, e->d_colidx, e->V}; }
+DevGraph graph(const p2pg_engine* e) {
+  return DevGraph{e->d_rowptr, e->d_colidx, e->d_rev, e->V};
+}
 
 // Timed launch: kernel class cls in [0,4).
 template <class F>
@@ -181,6 +190,13 @@ int alloc_state(p2pg_engine* e) {
     }
   }
   if ((rc = A((void**)&s.S, e->bm_bytes))) return rc;
+  if (gossip && e->d_rev && e->push_mode != 1) {
+    // dense-round edge-mask buffer, only if it fits with headroom (else row atomics only)
+    const size_t eb = (size_t)e->nnz * e->W * sizeof(uint64_t);
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && eb + ((size_t)4 << 30) < free_b)
+      if ((rc = A((void**)&s.E, eb ? eb : 8))) return rc;
+  }
   if (rec) {
     const size_t hb = (size_t)e->V * e->M * sizeof(int32_t);
     if ((rc = A((void**)&s.hop, hb))) return rc;
@@ -211,6 +227,9 @@ int p2pg_create(const p2pg_config* cfg, p2pg_engine** out) {
     return fail(nullptr, P2PG_ERR_ARG, "create: device ordinal out of range");
   p2pg_engine* e = new p2pg_engine;
   e->cfg = *cfg;
+  if (const char* t = std::getenv("P2PG_E_THRESH")) e->e_thresh = std::atof(t);
+  if (const char* m = std::getenv("P2PG_GOSSIP_PUSH"))
+    e->push_mode = !std::strcmp(m, "atomic") ? 1 : (!std::strcmp(m, "store") ? 2 : 0);
   HIPCHK(e, hipSetDevice(cfg->device));
   HIPCHK(e, hipStreamCreateWithFlags(&e->own_stream, hipStreamNonBlocking));
   e->stream = e->own_stream;
@@ -245,11 +264,34 @@ int p2pg_load_csr(p2pg_engine* e, int64_t V, const int64_t* rowptr, const int32_
         return fail(e, P2PG_ERR_GRAPH, "load_csr: row not strictly ascending");
     }
   }
+  // symmetry (every connection relays both ways, node.py:75-78) and reverse slots
+  std::vector<uint32_t> rev(e->cfg.mode == P2PG_MODE_GOSSIP && nnz < 0xFFFFFFFFll ? nnz : 0);
+  int64_t asym = -1;
+#pragma omp parallel for schedule(dynamic, 4096)
+  for (int64_t u = 0; u < V; ++u) {
+    for (int64_t j = rowptr[u]; j < rowptr[u + 1]; ++j) {
+      const int64_t v = colidx[j];
+      const int32_t* b = colidx + rowptr[v];
+      const int32_t* en = colidx + rowptr[v + 1];
+      const int32_t* it = std::lower_bound(b, en, (int32_t)u);
+      if (it == en || *it != u) {
+#pragma omp critical
+        asym = u;
+      } else if (!rev.empty()) {
+        rev[j] = (uint32_t)(rowptr[v] + (it - b));
+      }
+    }
+  }
+  if (asym >= 0) return fail(e, P2PG_ERR_GRAPH, "load_csr: adjacency not symmetric");
   HIPCHK(e, hipSetDevice(e->cfg.device));
   free_graph(e);
   free_state(e);
   e->V = V;
   e->nnz = nnz;
+  if (!rev.empty()) {
+    HIPCHK(e, hipMalloc((void**)&e->d_rev, sizeof(uint32_t) * rev.size()));
+    HIPCHK(e, hipMemcpy(e->d_rev, rev.data(), sizeof(uint32_t) * rev.size(), hipMemcpyHostToDevice));
+  }
   e->h_rowptr.assign(rowptr, rowptr + V + 1);
   HIPCHK(e, hipMalloc((void**)&e->d_rowptr, sizeof(int64_t) * (V + 1)));
   HIPCHK(e, hipMalloc((void**)&e->d_colidx, sizeof(int32_t) * (nnz ? nnz : 1)));
@@ -311,6 +353,7 @@ int p2pg_reset(p2pg_engine* e) {
   }
   e->round = 0;
   e->done = false;
+  e->last_push_e = false;
   for (int i = 0; i < 4; ++i) {
     e->kms[i] = 0;
     e->klaunch[i] = 0;
@@ -361,31 +404,54 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
     }
   } else if (!gossip) {
     if ((rc = timed(e, 1, [&] { return launch_flood_pull(g, s, p, e->stream); }))) return rc;
+  } else if (e->last_push_e) {
+    // previous round stored per-edge masks: gather them (pull, no atomics)
+    if ((rc = timed(e, 0, [&] { return launch_gossip_pull(g, s, p, e->stream); }))) return rc;
   } else {
     if ((rc = timed(e, 0, [&] { return launch_gossip_update(g, s, p, e->stream); }))) return rc;
   }
   if (s.hop)
     if ((rc = timed(e, 3, [&] { return launch_record(g, s, p, e->stream); }))) return rc;
-  if (gossip)
+  uint64_t tot[STAT_N] = {0};
+  auto read_stats = [&]() -> int {
+    HIPCHK(e, hipMemcpyAsync(e->h_stats, s.stats, sizeof(unsigned long long) * STAT_N * STAT_SHARDS,
+                             hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    int r2 = resolve_timings(e);
+    if (r2) return r2;
+    for (int i = 0; i < STAT_N; ++i) tot[i] = 0;
+    for (int sh = 0; sh < STAT_SHARDS; ++sh)
+      for (int i = 0; i < STAT_N; ++i) tot[i] += e->h_stats[sh * STAT_N + i];
+    if (e->round == 0) {
+      tot[ST_NEW] = host_new;
+      tot[ST_RELAYS] = host_relays;
+      tot[ST_ACTIVE_V] = host_av;
+      tot[ST_ACTIVE_W] = host_aw;
+      tot[ST_WEDGES] = host_wedge;
+      tot[ST_DEG_ACT] = host_degact;
+    }
+    return P2PG_OK;
+  };
+  if (gossip) {
+    // push form for this round's sends: row atomics when the frontier is sparse, whole-row
+    // edge-mask stores (+ pull next round) when most words of the active rows are set
+    bool use_e = false;
+    if (s.E) {
+      if (e->push_mode == 2) {
+        use_e = true;
+      } else if (e->push_mode == 0) {
+        if ((rc = read_stats())) return rc;
+        use_e = (double)tot[ST_ACTIVE_W] >=
+                e->e_thresh * (double)tot[ST_ACTIVE_V] * (double)e->W && tot[ST_ACTIVE_V] > 0;
+      }
+    }
     if ((rc = timed(e, 2, [&] {
-           return launch_gossip_scatter(g, s, p, e->d_hub, e->n_hub, e->stream);
+           return launch_gossip_scatter(g, s, p, e->d_hub, e->n_hub, use_e, e->stream);
          })))
       return rc;
-  HIPCHK(e, hipMemcpyAsync(e->h_stats, s.stats, sizeof(unsigned long long) * STAT_N * STAT_SHARDS,
-                           hipMemcpyDeviceToHost, e->stream));
-  HIPCHK(e, hipStreamSynchronize(e->stream));
-  if ((rc = resolve_timings(e))) return rc;
-  uint64_t tot[STAT_N] = {0};
-  for (int sh = 0; sh < STAT_SHARDS; ++sh)
-    for (int i = 0; i < STAT_N; ++i) tot[i] += e->h_stats[sh * STAT_N + i];
-  if (e->round == 0) {
-    tot[ST_NEW] = host_new;
-    tot[ST_RELAYS] = host_relays;
-    tot[ST_ACTIVE_V] = host_av;
-    tot[ST_ACTIVE_W] = host_aw;
-    tot[ST_WEDGES] = host_wedge;
-    tot[ST_DEG_ACT] = host_degact;
+    e->last_push_e = use_e;
   }
+  if ((rc = read_stats())) return rc;
   const bool active = tot[ST_NEW] != 0;
   if (out) {
     out->round = e->round;

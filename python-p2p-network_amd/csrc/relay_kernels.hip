@@ -83,18 +83,23 @@ __global__ void k_seed(DevState st, const int32_t* src, int32_t M) {
 }
 
 // ---------------------------------------------------------------------------------------
-// Flood, round r >= 1, pull form: for every unsaturated peer u, OR the round-(r-1) frontier
-// rows of its active neighbours (arrivals of round r), mask with ~seen (dedup), write the new
-// frontier row.  Reads only -- no atomics on the planes (row atomics measured 4x slower than
-// row reads on MI355X).  Lanes whose word is already full skip their loads.
-template <bool CHURN>
-__global__ __launch_bounds__(256) void k_flood_pull(DevGraph g, DevState st, RoundParams p) {
+// Pull form of a round r >= 1, shared by
+//   flood  (GOSSIP = false): sources are the round-(r-1) frontier rows F[(r-1)&1][v] of the
+//          active neighbours v (a flood sends the whole new set to every connection);
+//   gossip (GOSSIP = true):  sources are the per-edge masks E[rev(e)] that the active
+//          neighbours stored in round r-1 (dense rounds, see k_gossip_scatter<STORE_E>).
+// For every unsaturated peer u: OR the source rows (arrivals of round r), mask with ~seen
+// (dedup), write the new frontier row and A bit.  Reads only -- no atomics (row atomics
+// measured 4x slower than row reads on MI355X).  Lanes whose word is full skip their loads;
+// up to 8 neighbour rows are in flight per wave.
+template <bool CHURN, bool GOSSIP>
+__global__ __launch_bounds__(256) void k_pull(DevGraph g, DevState st, RoundParams p) {
   const int lane = threadIdx.x & 63;
   const int wib = wave_in_block();
   const int64_t V = g.V;
   const int W = st.W;
   const int cur = p.round & 1, prv = cur ^ 1;
-  const uint64_t* __restrict__ Fp = st.F[prv];
+  const uint64_t* __restrict__ Src = GOSSIP ? st.E : st.F[prv];
   uint64_t* __restrict__ Fc = st.F[cur];
   const uint32_t* __restrict__ Ap = st.A[prv];
   const int64_t ntasks = (V + 31) >> 5;
@@ -115,6 +120,8 @@ __global__ __launch_bounds__(256) void k_flood_pull(DevGraph g, DevState st, Rou
       const int64_t u = u0 + b;
       const int64_t beg = g.rowptr[u], end = g.rowptr[u + 1];
       const uint64_t deg = (uint64_t)(end - beg);
+      const uint64_t per_bit = GOSSIP ? (deg < (uint64_t)p.fanout ? deg : (uint64_t)p.fanout)
+                                      : deg - 1;
       bool row_new = false, row_full = true;
       for (int sl = 0; sl < nslices; ++sl) {
         const int w = sl * 64 + lane;
@@ -126,32 +133,35 @@ __global__ __launch_bounds__(256) void k_flood_pull(DevGraph g, DevState st, Rou
         if (__ballot(need != 0ull)) {
           for (int64_t cb = beg; cb < end; cb += 64) {
             const int64_t j = cb + lane;
-            int32_t v = 0;
+            uint32_t srow = 0;
             bool act = false;
             if (j < end) {
-              v = g.colidx[j];
+              const int32_t v = g.colidx[j];
               act = bit_test(Ap, v);
               if (CHURN && act)
                 act = !churn_dropped((uint32_t)(p.round - 1), (uint32_t)u, (uint32_t)v,
                                      p.churn_thr, p.cseed_lo, p.cseed_hi);
+              srow = GOSSIP ? g.rev[j] : (uint32_t)v;
             }
             uint64_t m = __ballot(act);
             while (m) {
-              int32_t vv[8];
+              uint32_t sv[8];
+              bool ok[8];
 #pragma unroll
               for (int k = 0; k < 8; ++k) {
+                ok[k] = m != 0ull;
                 if (m) {
                   const int idx = __builtin_ctzll(m);
                   m &= m - 1ull;
-                  vv[k] = __builtin_amdgcn_readlane(v, idx);
+                  sv[k] = (uint32_t)__builtin_amdgcn_readlane((int)srow, idx);
                 } else {
-                  vv[k] = -1;
+                  sv[k] = 0u;
                 }
               }
               uint64_t x[8];
 #pragma unroll
               for (int k = 0; k < 8; ++k)
-                x[k] = (vv[k] >= 0 && need) ? Fp[(int64_t)vv[k] * W + w] : 0ull;
+                x[k] = (ok[k] && need) ? Src[(int64_t)sv[k] * W + w] : 0ull;
 #pragma unroll
               for (int k = 0; k < 8; ++k) acc |= x[k];
             }
@@ -168,7 +178,7 @@ __global__ __launch_bounds__(256) void k_flood_pull(DevGraph g, DevState st, Rou
         if (nw) {
           const uint64_t pc = (uint64_t)__popcll(nw);
           c[ST_NEW] += pc;
-          c[ST_RELAYS] += pc * (deg - 1);
+          c[ST_RELAYS] += pc * per_bit;
           c[ST_ACTIVE_W] += 1;
           c[ST_WEDGES] += deg;
         }
@@ -191,9 +201,9 @@ __global__ __launch_bounds__(256) void k_flood_pull(DevGraph g, DevState st, Rou
 }
 
 // ---------------------------------------------------------------------------------------
-// Gossip, round r >= 1, part 1: consume the pushes of round r-1 (next[r&1], touched bitmap
-// T[r&1]), dedup against seen, write the round-r frontier row and A bit, clear what was
-// consumed.  Relays: min(k, deg) per first receipt.
+// Gossip, round r >= 1 after a sparse round: consume the row-atomic pushes of round r-1
+// (next[r&1], touched bitmap T[r&1]), dedup against seen, write the round-r frontier row and
+// A bit, clear what was consumed.  Relays: min(k, deg) per first receipt.
 __global__ __launch_bounds__(256) void k_gossip_update(DevGraph g, DevState st,
                                                         RoundParams p) {
   const int lane = threadIdx.x & 63;
@@ -257,15 +267,27 @@ __global__ __launch_bounds__(256) void k_gossip_update(DevGraph g, DevState st,
   flush_stats(st.stats, c, lane);
 }
 
-// Gossip, round r >= 0, part 2: every first receipt (v, m) of round r is pushed to k
-// Philox-chosen neighbours.  One wave per (source, GCHUNK-neighbour chunk):
-// each lane (= word) builds, in its own LDS column, the per-target masks of the chunk, then
-// every nonzero target mask goes out as one coalesced 512 B row atomicOr.
-template <bool CHURN, int K>
+// Orders this wave's LDS writes before its later LDS reads by other lanes.
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// Gossip, round r >= 0: every first receipt (v, m) of round r is pushed to k Philox-chosen
+// neighbours.  One wave per (source, GCHUNK-neighbour chunk):
+//   1. the row slice's active bits are compacted into an LDS list (prefix sum of popcounts),
+//      so the 64 lanes evaluate Philox + Floyd for equal shares of messages;
+//   2. picks landing in the chunk set bits of a GCHUNK x 64-word LDS mask table (LDS atomics);
+//   3. flush, lane = word: every (target, word) mask leaves as part of one 512 B row access --
+//      STORE_E = false (sparse rounds): row atomicOr into the target's next row + T bit;
+//      STORE_E = true  (dense rounds):  plain store of the whole row into the edge slot
+//      E[rowptr[v] + j] (zeros included), which the next round's k_pull<GOSSIP> gathers.
+template <bool CHURN, int K, bool STORE_E>
 __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st, RoundParams p,
                                                         const int64_t* __restrict__ hub_items,
                                                         int64_t n_hub) {
   __shared__ uint64_t tbl[WPB][GCHUNK][64];
+  __shared__ uint16_t lst[WPB][GLIST];
   const int lane = threadIdx.x & 63;
   const int wib = wave_in_block();
   const int64_t V = g.V;
@@ -307,47 +329,84 @@ __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st,
       const bool all = deg <= k;
       for (int sl = 0; sl < nslices; ++sl) {
         const int w = sl * 64 + lane;
-        const uint64_t f = w < W ? Fc[v * W + w] : 0ull;
-        if (!__ballot(f != 0ull)) continue;
-        if (!all) {
+        const bool valid = w < W;
+        const uint64_t f = valid ? Fc[v * W + w] : 0ull;
+        const bool anyf = __ballot(f != 0ull) != 0ull;
+        if (!anyf && !STORE_E) continue;
+        if (anyf && !all) {
           for (int j = 0; j < nn; ++j) tbl[wib][j][lane] = 0ull;
-          uint64_t rem = f;
-          while (rem) {
-            const int bit = __builtin_ctzll(rem);
-            rem &= rem - 1ull;
-            const uint32_t mg = p.msg_base + (uint32_t)(w * 64 + bit);
-            if constexpr (K > 0) {
-              uint32_t pk[K];
-              gossip_picks_t<K>((uint32_t)p.round, (uint32_t)v, mg, (uint32_t)deg, p.gseed_lo,
-                                p.gseed_hi, pk);
+          const uint32_t cnt = (uint32_t)__popcll(f);
+          uint32_t incl = cnt;
 #pragma unroll
-              for (int q = 0; q < K; ++q) {
-                const uint32_t jj = pk[q] - (uint32_t)nb;
-                if (jj < (uint32_t)nn) tbl[wib][jj][lane] |= 1ull << bit;
-              }
-            } else {
-              uint32_t pk[16];
-              gossip_picks((uint32_t)p.round, (uint32_t)v, mg, (uint32_t)deg, k, p.gseed_lo,
-                           p.gseed_hi, pk);
-              for (int q = 0; q < k; ++q) {
-                const uint32_t jj = pk[q] - (uint32_t)nb;
-                if (jj < (uint32_t)nn) tbl[wib][jj][lane] |= 1ull << bit;
+          for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t t = __shfl_up(incl, o);
+            if (lane >= o) incl += t;
+          }
+          const uint32_t excl = incl - cnt;
+          const uint32_t total = __shfl(incl, 63);
+          for (uint32_t lb = 0; lb < total; lb += GLIST) {
+            if (excl < lb + GLIST && excl + cnt > lb) {
+              uint64_t ff = f;
+              uint32_t rank = excl;
+              while (ff) {
+                const int bit = __builtin_ctzll(ff);
+                ff &= ff - 1ull;
+                if (rank >= lb && rank < lb + GLIST) lst[wib][rank - lb] = (uint16_t)((lane << 6) | bit);
+                ++rank;
               }
             }
+            wave_lds_sync();
+            const uint32_t n = total - lb < (uint32_t)GLIST ? total - lb : (uint32_t)GLIST;
+            for (uint32_t i = lane; i < n; i += 64) {
+              const uint32_t e = lst[wib][i];
+              const uint32_t wl = e >> 6, bit = e & 63u;
+              const uint32_t mg = p.msg_base + (uint32_t)((sl * 64 + (int)wl) * 64) + bit;
+              if constexpr (K > 0) {
+                uint32_t pk[K];
+                gossip_picks_t<K>((uint32_t)p.round, (uint32_t)v, mg, (uint32_t)deg, p.gseed_lo,
+                                  p.gseed_hi, pk);
+#pragma unroll
+                for (int q = 0; q < K; ++q) {
+                  const uint32_t jj = pk[q] - (uint32_t)nb;
+                  if (jj < (uint32_t)nn)
+                    atomicOr((unsigned long long*)&tbl[wib][jj][wl], 1ull << bit);
+                }
+              } else {
+                uint32_t pk[16];
+                gossip_picks((uint32_t)p.round, (uint32_t)v, mg, (uint32_t)deg, k, p.gseed_lo,
+                             p.gseed_hi, pk);
+                for (int q = 0; q < k; ++q) {
+                  const uint32_t jj = pk[q] - (uint32_t)nb;
+                  if (jj < (uint32_t)nn)
+                    atomicOr((unsigned long long*)&tbl[wib][jj][wl], 1ull << bit);
+                }
+              }
+            }
+            wave_lds_sync();
           }
         }
         for (int j = 0; j < nn; ++j) {
-          const uint64_t x = all ? f : tbl[wib][j][lane];
+          const uint64_t x = all ? f : (anyf ? tbl[wib][j][lane] : 0ull);
           const uint64_t bal = __ballot(x != 0ull);
-          if (!bal) continue;
-          const int32_t u = g.colidx[rb + nb + j];
-          if (CHURN && churn_dropped((uint32_t)p.round, (uint32_t)v, (uint32_t)u, p.churn_thr,
-                                     p.cseed_lo, p.cseed_hi))
-            continue;
-          if (x) atomicOr((unsigned long long*)&nx[(int64_t)u * W + w], (unsigned long long)x);
-          if (lane == 0) {
-            atomicOr(&Tn[u >> 5], 1u << (u & 31));
-            c[ST_SCATTER] += (uint64_t)__popcll(bal);
+          if (STORE_E) {
+            bool dropped = false;
+            if (CHURN && bal)
+              dropped = churn_dropped((uint32_t)p.round, (uint32_t)v,
+                                      (uint32_t)g.colidx[rb + nb + j], p.churn_thr, p.cseed_lo,
+                                      p.cseed_hi);
+            if (valid) st.E[(rb + nb + j) * W + w] = dropped ? 0ull : x;
+            if (!dropped && lane == 0) c[ST_SCATTER] += (uint64_t)__popcll(bal);
+          } else {
+            if (!bal) continue;
+            const int32_t u = g.colidx[rb + nb + j];
+            if (CHURN && churn_dropped((uint32_t)p.round, (uint32_t)v, (uint32_t)u, p.churn_thr,
+                                       p.cseed_lo, p.cseed_hi))
+              continue;
+            if (x) atomicOr((unsigned long long*)&nx[(int64_t)u * W + w], (unsigned long long)x);
+            if (lane == 0) {
+              atomicOr(&Tn[u >> 5], 1u << (u & 31));
+              c[ST_SCATTER] += (uint64_t)__popcll(bal);
+            }
           }
         }
       }
@@ -499,9 +558,16 @@ hipError_t launch_flood_pull(const DevGraph& g, const DevState& st, const RoundP
                              hipStream_t s) {
   const int grid = grid_tasks((g.V + 31) >> 5);
   if (p.churn_thr)
-    hipLaunchKernelGGL(k_flood_pull<true>, dim3(grid), dim3(256), 0, s, g, st, p);
+    hipLaunchKernelGGL((k_pull<true, false>), dim3(grid), dim3(256), 0, s, g, st, p);
   else
-    hipLaunchKernelGGL(k_flood_pull<false>, dim3(grid), dim3(256), 0, s, g, st, p);
+    hipLaunchKernelGGL((k_pull<false, false>), dim3(grid), dim3(256), 0, s, g, st, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_gossip_pull(const DevGraph& g, const DevState& st, const RoundParams& p,
+                              hipStream_t s) {
+  const int grid = grid_tasks((g.V + 31) >> 5);
+  hipLaunchKernelGGL((k_pull<false, true>), dim3(grid), dim3(256), 0, s, g, st, p);
   return hipGetLastError();
 }
 
@@ -512,11 +578,11 @@ hipError_t launch_gossip_update(const DevGraph& g, const DevState& st, const Rou
   return hipGetLastError();
 }
 
-hipError_t launch_gossip_scatter(const DevGraph& g, const DevState& st, const RoundParams& p,
-                                 const int64_t* hub_items, int64_t n_hub_items, hipStream_t s) {
-  const int grid = grid_tasks(((g.V + 31) >> 5) + n_hub_items);
+template <bool SE>
+void scatter_dispatch(int grid, const DevGraph& g, const DevState& st, const RoundParams& p,
+                      const int64_t* hub_items, int64_t n_hub_items, hipStream_t s) {
 #define P2PG_SCATTER(CH, KK)                                                                 \
-  hipLaunchKernelGGL((k_gossip_scatter<CH, KK>), dim3(grid), dim3(256), 0, s, g, st, p,      \
+  hipLaunchKernelGGL((k_gossip_scatter<CH, KK, SE>), dim3(grid), dim3(256), 0, s, g, st, p,  \
                      hub_items, n_hub_items)
   const bool ch = p.churn_thr != 0;
   switch (p.fanout) {
@@ -527,6 +593,16 @@ hipError_t launch_gossip_scatter(const DevGraph& g, const DevState& st, const Ro
     default: if (ch) P2PG_SCATTER(true, 0); else P2PG_SCATTER(false, 0); break;
   }
 #undef P2PG_SCATTER
+}
+
+hipError_t launch_gossip_scatter(const DevGraph& g, const DevState& st, const RoundParams& p,
+                                 const int64_t* hub_items, int64_t n_hub_items, bool store_e,
+                                 hipStream_t s) {
+  const int grid = grid_tasks(((g.V + 31) >> 5) + n_hub_items);
+  if (store_e)
+    scatter_dispatch<true>(grid, g, st, p, hub_items, n_hub_items, s);
+  else
+    scatter_dispatch<false>(grid, g, st, p, hub_items, n_hub_items, s);
   return hipGetLastError();
 }
 

@@ -247,3 +247,48 @@ def test_config4_gossip_full_size_parity():
     np.testing.assert_array_equal(hop, ora.hop)
     np.testing.assert_array_equal(parent, ora.parent)
     assert_rounds_equal(sub, ora.rounds)
+
+
+@pytest.mark.parametrize("push", ["atomic", "store", "auto"])
+@pytest.mark.parametrize("name", golden_cases())
+def test_gpu_gossip_push_forms_match_golden(name, push, monkeypatch):
+    """Both push forms (row atomics into next / edge-mask stores gathered by a pull) and the
+    automatic per-round switch give the reference-harness results bit for bit."""
+    z = load_golden(name)
+    if str(z["mode"]) != "gossip":
+        pytest.skip("flood case")
+    monkeypatch.setenv("P2PG_GOSSIP_PUSH", push)
+    monkeypatch.setenv("P2PG_E_THRESH", "0.05")  # let small graphs switch to stores in auto
+    with gpu_net(z, "gossip", int(z["fanout"]), int(z["gossip_seed"]), int(z["churn_threshold"]),
+                 int(z["churn_seed"])) as net:
+        net.broadcast(z["src"])
+        rounds = net.run()
+        hop, parent = net.hop_parent()
+    np.testing.assert_array_equal(hop, z["hop"])
+    np.testing.assert_array_equal(parent, z["parent"])
+    ora = oracle_for(z["rowptr"], z["colidx"], z["src"], "gossip", int(z["fanout"]), int(z["gossip_seed"]),
+                     int(z["churn_threshold"]), int(z["churn_seed"]))
+    assert_rounds_equal(rounds, ora.rounds)
+
+
+@pytest.mark.parametrize("push", ["atomic", "store"])
+@pytest.mark.parametrize("kind,p,M,thr,fanout", [
+    ("ba", dict(V=600, m=3), 64, 0, 3),
+    ("ws", dict(V=500, k=6, b=0.2), 200, 300_000_000, 2),
+    ("ba", dict(V=150, m=20), 4160, 0, 3),
+    ("gnp", dict(V=300, k=5.0), 130, 0, 7),
+])
+def test_gpu_gossip_push_forms_match_oracle(kind, p, M, thr, fanout, push, monkeypatch):
+    from p2pnetwork.gpu import make_sources
+    monkeypatch.setenv("P2PG_GOSSIP_PUSH", push)
+    seed = zlib.crc32(repr((kind, M, thr, fanout)).encode()) & 0xFFFF
+    g = make_graph(kind, p, seed)
+    src = make_sources(g.V, M, seed=seed + 3)
+    with gpu_net(g, "gossip", fanout, 99 + seed, thr, 5 + seed) as net:
+        net.broadcast(src)
+        rounds = net.run()
+        hop, parent = net.hop_parent()
+    ora = oracle_for(g.rowptr, g.colidx, src, "gossip", fanout, 99 + seed, thr, 5 + seed)
+    np.testing.assert_array_equal(hop, ora.hop)
+    np.testing.assert_array_equal(parent, ora.parent)
+    assert_rounds_equal(rounds, ora.rounds)
