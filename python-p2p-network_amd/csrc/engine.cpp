@@ -38,6 +38,13 @@ struct p2pg_engine {
   int64_t* d_hub = nullptr;
   int64_t n_hub = 0;
   uint32_t* d_rev = nullptr;   // gossip: reverse edge slots
+  // pull hub split (deg > HUB_T)
+  uint32_t* d_H = nullptr;
+  int64_t* d_hub_items = nullptr;
+  int32_t* d_hubs = nullptr;
+  int64_t* d_hub_begin = nullptr;
+  uint64_t* d_partial = nullptr;
+  HubPlan hp{};
   bool last_push_e = false;    // gossip: pushes of the previous round went to E (dense)
   double e_thresh = 0.1;       // store-mode when active words >= thresh * active rows * W
   int push_mode = 0;           // 0 auto, 1 always row atomics, 2 always edge stores
@@ -103,6 +110,12 @@ void free_graph(p2pg_engine* e) {
   dfree(e->d_colidx);
   dfree(e->d_hub);
   dfree(e->d_rev);
+  dfree(e->d_H);
+  dfree(e->d_hub_items);
+  dfree(e->d_hubs);
+  dfree(e->d_hub_begin);
+  dfree(e->d_partial);
+  e->hp = HubPlan{};
   e->n_hub = 0;
 }
 
@@ -121,7 +134,7 @@ RoundParams params(const p2pg_engine* e) {
 }
 
 DevGraph graph(const p2pg_engine* e) {
-  return DevGraph{e->d_rowptr, e->d_colidx, e->d_rev, e->V};
+  return DevGraph{e->d_rowptr, e->d_colidx, e->d_rev, e->d_H, e->V};
 }
 
 // Timed launch: kernel class cls in [0,4).
@@ -305,6 +318,32 @@ int p2pg_load_csr(p2pg_engine* e, int64_t V, const int64_t* rowptr, const int32_
       for (int64_t c = 0; c * GCHUNK < d; ++c) hub.push_back((v << 32) | c);
   }
   e->n_hub = (int64_t)hub.size();
+  {  // pull-side hub plan
+    std::vector<int32_t> hubs;
+    std::vector<int64_t> items, begin{0};
+    std::vector<uint32_t> H((V + 31) / 32, 0u);
+    for (int64_t v = 0; v < V; ++v) {
+      const int64_t d = rowptr[v + 1] - rowptr[v];
+      if (d <= HUB_T) continue;
+      hubs.push_back((int32_t)v);
+      H[v >> 5] |= 1u << (v & 31);
+      for (int64_t c = 0; c * HUB_CHUNK < d; ++c) items.push_back((v << 32) | c);
+      begin.push_back((int64_t)items.size());
+    }
+    HIPCHK(e, hipMalloc((void**)&e->d_H, sizeof(uint32_t) * H.size()));
+    HIPCHK(e, hipMemcpy(e->d_H, H.data(), sizeof(uint32_t) * H.size(), hipMemcpyHostToDevice));
+    if (!hubs.empty()) {
+      HIPCHK(e, hipMalloc((void**)&e->d_hubs, sizeof(int32_t) * hubs.size()));
+      HIPCHK(e, hipMalloc((void**)&e->d_hub_items, sizeof(int64_t) * items.size()));
+      HIPCHK(e, hipMalloc((void**)&e->d_hub_begin, sizeof(int64_t) * begin.size()));
+      HIPCHK(e, hipMalloc((void**)&e->d_partial, sizeof(uint64_t) * 64 * items.size()));
+      HIPCHK(e, hipMemcpy(e->d_hubs, hubs.data(), sizeof(int32_t) * hubs.size(), hipMemcpyHostToDevice));
+      HIPCHK(e, hipMemcpy(e->d_hub_items, items.data(), sizeof(int64_t) * items.size(), hipMemcpyHostToDevice));
+      HIPCHK(e, hipMemcpy(e->d_hub_begin, begin.data(), sizeof(int64_t) * begin.size(), hipMemcpyHostToDevice));
+    }
+    e->hp = HubPlan{e->d_hub_items, (int64_t)items.size(), e->d_hubs, e->d_hub_begin,
+                    (int64_t)hubs.size(), e->d_partial};
+  }
   HIPCHK(e, hipMalloc((void**)&e->d_hub, sizeof(int64_t) * (hub.empty() ? 1 : hub.size())));
   if (!hub.empty())
     HIPCHK(e, hipMemcpy(e->d_hub, hub.data(), sizeof(int64_t) * hub.size(), hipMemcpyHostToDevice));
@@ -403,10 +442,10 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
       host_wedge += (uint64_t)(e->h_rowptr[v + 1] - e->h_rowptr[v]);
     }
   } else if (!gossip) {
-    if ((rc = timed(e, 1, [&] { return launch_flood_pull(g, s, p, e->stream); }))) return rc;
+    if ((rc = timed(e, 1, [&] { return launch_flood_pull(g, s, p, e->hp, e->stream); }))) return rc;
   } else if (e->last_push_e) {
     // previous round stored per-edge masks: gather them (pull, no atomics)
-    if ((rc = timed(e, 0, [&] { return launch_gossip_pull(g, s, p, e->stream); }))) return rc;
+    if ((rc = timed(e, 0, [&] { return launch_gossip_pull(g, s, p, e->hp, e->stream); }))) return rc;
   } else {
     if ((rc = timed(e, 0, [&] { return launch_gossip_update(g, s, p, e->stream); }))) return rc;
   }

@@ -86,8 +86,9 @@ __global__ void k_seed(DevState st, const int32_t* src, int32_t M) {
 // Pull form of a round r >= 1, shared by
 //   flood  (GOSSIP = false): sources are the round-(r-1) frontier rows F[(r-1)&1][v] of the
 //          active neighbours v (a flood sends the whole new set to every connection);
-//   gossip (GOSSIP = true):  sources are the per-edge masks E[rev(e)] that the active
-//          neighbours stored in round r-1 (dense rounds, see k_gossip_scatter<STORE_E>).
+//   gossip (GOSSIP = true):  sources are the per-connection masks E[slot] (receiver-major:
+//          slot = u's own CSR slot of the connection) that the active neighbours stored in
+//          round r-1 (dense rounds, see k_gossip_scatter<STORE_E>).
 // For every unsaturated peer u: OR the source rows (arrivals of round r), mask with ~seen
 // (dedup), write the new frontier row and A bit.  Reads only -- no atomics (row atomics
 // measured 4x slower than row reads on MI355X).  Lanes whose word is full skip their loads;
@@ -141,7 +142,7 @@ __global__ __launch_bounds__(256) void k_pull(DevGraph g, DevState st, RoundPara
               if (CHURN && act)
                 act = !churn_dropped((uint32_t)(p.round - 1), (uint32_t)u, (uint32_t)v,
                                      p.churn_thr, p.cseed_lo, p.cseed_hi);
-              srow = GOSSIP ? g.rev[j] : (uint32_t)v;
+              srow = GOSSIP ? (uint32_t)j : (uint32_t)v;
             }
             uint64_t m = __ballot(act);
             while (m) {
@@ -196,6 +197,287 @@ __global__ __launch_bounds__(256) void k_pull(DevGraph g, DevState st, RoundPara
       st.A[cur][task] = aw;
       if (sat != sat0) st.S[task] = sat;
     }
+  }
+  flush_stats(st.stats, c, lane);
+}
+
+__device__ __forceinline__ int64_t readlane64(int64_t x, int l) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)x >> 32), l);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+// One target's prefetch stage for k_pull1: row range, seen word, first 64 neighbour slots.
+struct PullStage {
+  int b;            // target index in the task (-1 = none)
+  int64_t beg, end; // slot range
+  uint64_t s;       // this lane's seen word
+  int32_t v;        // this lane's neighbour (first chunk)
+  uint32_t r;       // its source row (flood: v, gossip: the slot itself)
+  bool act;         // neighbour active (and its send not lost)
+};
+
+// Same computation as k_pull for W <= 64 (one row slice), software-pipelined two targets
+// deep so that a target costs ~one memory round trip instead of five: the task's 33 row
+// offsets come in one load; target t+2's seen word and first neighbour chunk are issued, and
+// target t+1's activity gather (A bits of its neighbours) is issued, before target t's rows
+// are loaded, and all three wait together.  Hub targets (g.H) are left to k_pull_hub_*.
+template <bool CHURN, bool GOSSIP>
+__global__ __launch_bounds__(256) void k_pull1(DevGraph g, DevState st, RoundParams p) {
+  const int lane = threadIdx.x & 63;
+  const int wib = wave_in_block();
+  const int64_t V = g.V;
+  const int W = st.W;
+  const int cur = p.round & 1, prv = cur ^ 1;
+  const uint64_t* __restrict__ Src = GOSSIP ? st.E : st.F[prv];
+  uint64_t* __restrict__ Fc = st.F[cur];
+  const uint32_t* __restrict__ Ap = st.A[prv];
+  const int64_t ntasks = (V + 31) >> 5;
+  const bool valid = lane < W;
+  const uint64_t fm = valid ? full_mask(lane, W, st.M) : 0ull;
+  uint64_t c[STAT_N] = {0, 0, 0, 0, 0, 0, 0, 0};
+
+  for (int64_t task = (int64_t)blockIdx.x * WPB + wib; task < ntasks;
+       task += (int64_t)gridDim.x * WPB) {
+    const int64_t u0 = task << 5;
+    const uint32_t sat0 = st.S[task];
+    uint32_t todo = ~sat0;
+    if (g.H) todo &= ~g.H[task];  // hubs: k_pull_hub_* items
+    if (V - u0 < 32) todo &= (1u << (V - u0)) - 1u;
+    if (!todo) {
+      if (lane == 0) st.A[cur][task] = 0u;
+      continue;
+    }
+    int64_t rp = 0;
+    if (lane <= 32 && u0 + lane <= V) rp = g.rowptr[u0 + lane];
+
+    auto issue = [&](PullStage& q, int b) {
+      q.b = b;
+      q.act = false;
+      q.v = 0;
+      q.r = 0;
+      q.s = 0;
+      if (b < 0) return;
+      q.beg = readlane64(rp, b);
+      q.end = readlane64(rp, b + 1);
+      if (valid) q.s = st.seen[(u0 + b) * W + lane];
+      const int64_t j = q.beg + lane;
+      if (j < q.end) {
+        q.v = g.colidx[j];
+        q.r = GOSSIP ? (uint32_t)j : (uint32_t)q.v;
+      }
+    };
+    auto activity = [&](PullStage& q) {
+      if (q.b < 0) return;
+      const int64_t j = q.beg + lane;
+      bool a = false;
+      if (j < q.end) {
+        a = bit_test(Ap, q.v);
+        if (CHURN && a)
+          a = !churn_dropped((uint32_t)(p.round - 1), (uint32_t)(u0 + q.b), (uint32_t)q.v,
+                             p.churn_thr, p.cseed_lo, p.cseed_hi);
+      }
+      q.act = a;
+    };
+    auto next_bit = [](uint32_t& t) -> int {
+      if (!t) return -1;
+      const int b = __builtin_ctz(t);
+      t &= t - 1u;
+      return b;
+    };
+
+    uint32_t rest = todo;
+    PullStage s1, s2, s3;
+    issue(s1, next_bit(rest));
+    issue(s2, next_bit(rest));
+    activity(s1);
+    uint32_t aw = 0, sat = sat0;
+    while (s1.b >= 0) {
+      issue(s3, next_bit(rest));
+      activity(s2);
+      const int64_t u = u0 + s1.b;
+      const uint64_t deg = (uint64_t)(s1.end - s1.beg);
+      const uint64_t need = fm & ~s1.s;
+      uint64_t acc = 0;
+      if (__ballot(need != 0ull)) {
+        uint64_t m = __ballot(s1.act);
+        uint32_t srow = s1.r;
+        int64_t cb = s1.beg;
+        for (;;) {
+          while (m) {
+            uint32_t sv[8];
+            bool ok[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              ok[k] = m != 0ull;
+              if (m) {
+                const int idx = __builtin_ctzll(m);
+                m &= m - 1ull;
+                sv[k] = (uint32_t)__builtin_amdgcn_readlane((int)srow, idx);
+              } else {
+                sv[k] = 0u;
+              }
+            }
+            uint64_t x[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+              x[k] = (ok[k] && need) ? Src[(int64_t)sv[k] * W + lane] : 0ull;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc |= x[k];
+          }
+          cb += 64;
+          if (cb >= s1.end) break;
+          const int64_t j = cb + lane;  // further chunks of a wide row: serial
+          bool a = false;
+          srow = 0;
+          if (j < s1.end) {
+            const int32_t v = g.colidx[j];
+            srow = GOSSIP ? (uint32_t)j : (uint32_t)v;
+            a = bit_test(Ap, v);
+            if (CHURN && a)
+              a = !churn_dropped((uint32_t)(p.round - 1), (uint32_t)u, (uint32_t)v, p.churn_thr,
+                                 p.cseed_lo, p.cseed_hi);
+          }
+          m = __ballot(a);
+        }
+      }
+      const uint64_t nw = acc & need;
+      const bool any = __ballot(nw != 0ull) != 0ull;
+      if (nw) {
+        st.seen[u * W + lane] = s1.s | nw;
+        const uint64_t pc = (uint64_t)__popcll(nw);
+        const uint64_t per_bit = GOSSIP ? (deg < (uint64_t)p.fanout ? deg : (uint64_t)p.fanout)
+                                        : deg - 1;
+        c[ST_NEW] += pc;
+        c[ST_RELAYS] += pc * per_bit;
+        c[ST_ACTIVE_W] += 1;
+        c[ST_WEDGES] += deg;
+      }
+      if (any) {
+        if (valid) Fc[u * W + lane] = nw;
+        aw |= 1u << s1.b;
+        if (lane == 0) {
+          c[ST_ACTIVE_V] += 1;
+          c[ST_DEG_ACT] += deg;
+        }
+      }
+      if (!__ballot(valid && (s1.s | nw) != fm)) sat |= 1u << s1.b;
+      s1 = s2;
+      s2 = s3;
+    }
+    if (lane == 0) {
+      st.A[cur][task] = aw;
+      if (sat != sat0) st.S[task] = sat;
+    }
+  }
+  flush_stats(st.stats, c, lane);
+}
+
+// Hub targets of the pull (deg > HUB_T), part 1: one wave per (hub, HUB_CHUNK-slot chunk)
+// ORs that chunk's active source rows into a partial row.
+template <bool CHURN, bool GOSSIP>
+__global__ __launch_bounds__(256) void k_pull_hub_partial(DevGraph g, DevState st,
+                                                          RoundParams p, HubPlan hp) {
+  const int lane = threadIdx.x & 63;
+  const int wib = wave_in_block();
+  const int W = st.W;
+  const int prv = (p.round & 1) ^ 1;
+  const uint64_t* __restrict__ Src = GOSSIP ? st.E : st.F[prv];
+  const uint32_t* __restrict__ Ap = st.A[prv];
+  const bool valid = lane < W;
+  const uint64_t fm = valid ? full_mask(lane, W, st.M) : 0ull;
+  for (int64_t it = (int64_t)blockIdx.x * WPB + wib; it < hp.n_items;
+       it += (int64_t)gridDim.x * WPB) {
+    const int64_t packed = hp.items[it];
+    const int64_t u = packed >> 32;
+    const int64_t chunk = packed & 0xFFFFFFFFll;
+    const int64_t rb = g.rowptr[u], re = g.rowptr[u + 1];
+    const int64_t beg = rb + chunk * HUB_CHUNK;
+    const int64_t end = beg + HUB_CHUNK < re ? beg + HUB_CHUNK : re;
+    const uint64_t need = valid ? fm & ~st.seen[u * W + lane] : 0ull;
+    uint64_t acc = 0;
+    if (__ballot(need != 0ull) && !bit_test(st.S, u)) {
+      for (int64_t cb = beg; cb < end; cb += 64) {
+        const int64_t j = cb + lane;
+        uint32_t srow = 0;
+        bool a = false;
+        if (j < end) {
+          const int32_t v = g.colidx[j];
+          srow = GOSSIP ? (uint32_t)j : (uint32_t)v;
+          a = bit_test(Ap, v);
+          if (CHURN && a)
+            a = !churn_dropped((uint32_t)(p.round - 1), (uint32_t)u, (uint32_t)v, p.churn_thr,
+                               p.cseed_lo, p.cseed_hi);
+        }
+        uint64_t m = __ballot(a);
+        while (m) {
+          uint32_t sv[8];
+          bool ok[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            ok[k] = m != 0ull;
+            if (m) {
+              const int idx = __builtin_ctzll(m);
+              m &= m - 1ull;
+              sv[k] = (uint32_t)__builtin_amdgcn_readlane((int)srow, idx);
+            } else {
+              sv[k] = 0u;
+            }
+          }
+          uint64_t x[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+            x[k] = (ok[k] && need) ? Src[(int64_t)sv[k] * W + lane] : 0ull;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) acc |= x[k];
+        }
+      }
+    }
+    hp.partial[it * 64 + lane] = acc;
+  }
+}
+
+// Hub targets, part 2: one wave per hub ORs its partial rows, dedups against seen and writes
+// the frontier row; A / S bits by atomicOr (the main pull kernel stored those words whole).
+template <bool GOSSIP>
+__global__ __launch_bounds__(256) void k_pull_hub_finalize(DevGraph g, DevState st,
+                                                           RoundParams p, HubPlan hp) {
+  const int lane = threadIdx.x & 63;
+  const int wib = wave_in_block();
+  const int W = st.W;
+  const int cur = p.round & 1;
+  const bool valid = lane < W;
+  const uint64_t fm = valid ? full_mask(lane, W, st.M) : 0ull;
+  uint64_t c[STAT_N] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int64_t h = (int64_t)blockIdx.x * WPB + wib; h < hp.n_hubs;
+       h += (int64_t)gridDim.x * WPB) {
+    const int64_t u = hp.hubs[h];
+    if (bit_test(st.S, u)) continue;
+    uint64_t acc = 0;
+    for (int64_t it = hp.item_begin[h]; it < hp.item_begin[h + 1]; ++it)
+      acc |= hp.partial[it * 64 + lane];
+    const uint64_t s = valid ? st.seen[u * W + lane] : 0ull;
+    const uint64_t nw = acc & fm & ~s;
+    const uint64_t deg = (uint64_t)(g.rowptr[u + 1] - g.rowptr[u]);
+    if (nw) {
+      st.seen[u * W + lane] = s | nw;
+      const uint64_t pc = (uint64_t)__popcll(nw);
+      const uint64_t per_bit = GOSSIP ? (deg < (uint64_t)p.fanout ? deg : (uint64_t)p.fanout)
+                                      : deg - 1;
+      c[ST_NEW] += pc;
+      c[ST_RELAYS] += pc * per_bit;
+      c[ST_ACTIVE_W] += 1;
+      c[ST_WEDGES] += deg;
+    }
+    if (__ballot(nw != 0ull)) {
+      if (valid) st.F[cur][u * W + lane] = nw;
+      if (lane == 0) {
+        atomicOr(&st.A[cur][u >> 5], 1u << (u & 31));
+        c[ST_ACTIVE_V] += 1;
+        c[ST_DEG_ACT] += deg;
+      }
+    }
+    if (!__ballot(valid && (s | nw) != fm) && lane == 0) atomicOr(&st.S[u >> 5], 1u << (u & 31));
   }
   flush_stats(st.stats, c, lane);
 }
@@ -280,13 +562,15 @@ __device__ __forceinline__ void wave_lds_sync() {
 //   2. picks landing in the chunk set bits of a GCHUNK x 64-word LDS mask table (LDS atomics);
 //   3. flush, lane = word: every (target, word) mask leaves as part of one 512 B row access --
 //      STORE_E = false (sparse rounds): row atomicOr into the target's next row + T bit;
-//      STORE_E = true  (dense rounds):  plain store of the whole row into the edge slot
-//      E[rowptr[v] + j] (zeros included), which the next round's k_pull<GOSSIP> gathers.
+//      STORE_E = true  (dense rounds):  plain store of the whole row (zeros included) into
+//      E[rev(slot)], the receiver's own slot of the connection, which the next round's
+//      k_pull1<GOSSIP> then streams contiguously per receiver.
 template <bool CHURN, int K, bool STORE_E>
 __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st, RoundParams p,
                                                         const int64_t* __restrict__ hub_items,
                                                         int64_t n_hub) {
-  __shared__ uint64_t tbl[WPB][GCHUNK][64];
+  // row stride 65 words: lanes ORing the same word into different targets hit different banks
+  __shared__ uint64_t tbl[WPB][GCHUNK][65];
   __shared__ uint16_t lst[WPB][GLIST];
   const int lane = threadIdx.x & 63;
   const int wib = wave_in_block();
@@ -385,6 +669,8 @@ __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st,
             wave_lds_sync();
           }
         }
+        uint32_t rv = 0;  // receiver-side slots of this chunk's connections (lane j)
+        if (STORE_E && lane < nn) rv = g.rev[rb + nb + lane];
         for (int j = 0; j < nn; ++j) {
           const uint64_t x = all ? f : (anyf ? tbl[wib][j][lane] : 0ull);
           const uint64_t bal = __ballot(x != 0ull);
@@ -394,7 +680,10 @@ __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st,
               dropped = churn_dropped((uint32_t)p.round, (uint32_t)v,
                                       (uint32_t)g.colidx[rb + nb + j], p.churn_thr, p.cseed_lo,
                                       p.cseed_hi);
-            if (valid) st.E[(rb + nb + j) * W + w] = dropped ? 0ull : x;
+            // receiver-major: the row lands in the RECEIVER's slot for this connection, so
+            // the pull streams its own contiguous slot range
+            const uint32_t dslot = (uint32_t)__builtin_amdgcn_readlane((int)rv, j);
+            if (valid) st.E[(int64_t)dslot * W + w] = dropped ? 0ull : x;
             if (!dropped && lane == 0) c[ST_SCATTER] += (uint64_t)__popcll(bal);
           } else {
             if (!bal) continue;
@@ -554,21 +843,35 @@ hipError_t launch_seed(const DevState& st, const int32_t* src, int32_t M, hipStr
   return hipGetLastError();
 }
 
-hipError_t launch_flood_pull(const DevGraph& g, const DevState& st, const RoundParams& p,
-                             hipStream_t s) {
+template <bool CHURN, bool GOSSIP>
+hipError_t pull_with_hubs(const DevGraph& g, const DevState& st, const RoundParams& p,
+                          const HubPlan& hp, hipStream_t s) {
   const int grid = grid_tasks((g.V + 31) >> 5);
-  if (p.churn_thr)
-    hipLaunchKernelGGL((k_pull<true, false>), dim3(grid), dim3(256), 0, s, g, st, p);
-  else
-    hipLaunchKernelGGL((k_pull<false, false>), dim3(grid), dim3(256), 0, s, g, st, p);
+  if (st.W <= 64) {
+    if (hp.n_items)
+      hipLaunchKernelGGL((k_pull_hub_partial<CHURN, GOSSIP>), dim3(grid_tasks(hp.n_items)),
+                         dim3(256), 0, s, g, st, p, hp);
+    hipLaunchKernelGGL((k_pull1<CHURN, GOSSIP>), dim3(grid), dim3(256), 0, s, g, st, p);
+    if (hp.n_hubs)
+      hipLaunchKernelGGL((k_pull_hub_finalize<GOSSIP>), dim3(grid_tasks(hp.n_hubs)), dim3(256),
+                         0, s, g, st, p, hp);
+  } else {
+    DevGraph g2 = g;
+    g2.H = nullptr;  // multi-slice rows: no hub split
+    hipLaunchKernelGGL((k_pull<CHURN, GOSSIP>), dim3(grid), dim3(256), 0, s, g2, st, p);
+  }
   return hipGetLastError();
 }
 
+hipError_t launch_flood_pull(const DevGraph& g, const DevState& st, const RoundParams& p,
+                             const HubPlan& hp, hipStream_t s) {
+  return p.churn_thr ? pull_with_hubs<true, false>(g, st, p, hp, s)
+                     : pull_with_hubs<false, false>(g, st, p, hp, s);
+}
+
 hipError_t launch_gossip_pull(const DevGraph& g, const DevState& st, const RoundParams& p,
-                              hipStream_t s) {
-  const int grid = grid_tasks((g.V + 31) >> 5);
-  hipLaunchKernelGGL((k_pull<false, true>), dim3(grid), dim3(256), 0, s, g, st, p);
-  return hipGetLastError();
+                              const HubPlan& hp, hipStream_t s) {
+  return pull_with_hubs<false, true>(g, st, p, hp, s);
 }
 
 hipError_t launch_gossip_update(const DevGraph& g, const DevState& st, const RoundParams& p,

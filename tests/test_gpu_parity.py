@@ -92,6 +92,9 @@ CASES = [
     ("ba", dict(V=400, m=5), "gossip", 64, 900_000_000),
     ("gnp", dict(V=200, k=8.0), "flood", 4160, 0),         # W = 65: multi-slice rows
     ("ba", dict(V=150, m=20), "gossip", 4160, 0),          # hubs > 1 chunk, W = 65
+    ("hub", dict(V=1500, m=3, star=1100), "flood", 64, 0),  # pull hub split (deg > 512)
+    ("hub", dict(V=1500, m=3, star=1100), "gossip", 128, 0),
+    ("hub", dict(V=1500, m=3, star=1100), "flood", 100, 500_000_000),
 ]
 
 
@@ -103,6 +106,13 @@ def make_graph(kind, p, seed):
         return PeerGraph.gnp(p["V"], p["k"], seed)
     if kind == "ba":
         return PeerGraph.barabasi_albert(p["V"], p["m"], seed)
+    if kind == "hub":  # power-law graph plus two stars wider than the pull hub threshold
+        g = PeerGraph.barabasi_albert(p["V"], p["m"], seed)
+        rows = np.repeat(np.arange(g.V), g.degree())
+        e = [(int(a), int(b)) for a, b in zip(rows, g.colidx) if a < b]
+        e += [(7, j) for j in range(100, 100 + p["star"])]
+        e += [(1499, j) for j in range(0, 1400, 2)]
+        return PeerGraph.from_edges(g.V, e)
     return PeerGraph.watts_strogatz(p["V"], p["k"], p["b"], seed)
 
 
@@ -273,6 +283,7 @@ def test_gpu_gossip_push_forms_match_golden(name, push, monkeypatch):
 
 @pytest.mark.parametrize("push", ["atomic", "store"])
 @pytest.mark.parametrize("kind,p,M,thr,fanout", [
+    ("hub", dict(V=1500, m=3, star=1100), 64, 0, 3),
     ("ba", dict(V=600, m=3), 64, 0, 3),
     ("ws", dict(V=500, k=6, b=0.2), 200, 300_000_000, 2),
     ("ba", dict(V=150, m=20), 4160, 0, 3),

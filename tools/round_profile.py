@@ -17,6 +17,7 @@ from p2pnetwork.gpu import GraphNetwork, make_sources  # noqa: E402
 
 def main():
     wl = sys.argv[1] if len(sys.argv) > 1 else "c4"
+    runs = int(sys.argv[2]) if len(sys.argv) > 2 else 2
     w = bench.WORKLOADS[wl]
     g = bench.build_graph(w)
     src = make_sources(g.V, w["M"], seed=1)
@@ -24,7 +25,7 @@ def main():
         net.broadcast(src)
         net.run()
         out = []
-        for i in range(2):
+        for i in range(runs):
             net.reset()
             t = time.perf_counter()
             rounds = []
