@@ -619,25 +619,34 @@ __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st,
         if (!anyf && !STORE_E) continue;
         if (anyf && !all) {
           for (int j = 0; j < nn; ++j) tbl[wib][j][lane] = 0ull;
+          // rank-major compaction: list = every word's 1st set bit, then every word's 2nd
+          // set bit, ... so a 64-entry batch covers ~64 distinct words (distinct LDS table
+          // columns -> few bank conflicts), while every lane still gets equal work
           const uint32_t cnt = (uint32_t)__popcll(f);
-          uint32_t incl = cnt;
+          uint32_t maxc = cnt;
 #pragma unroll
-          for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t t = __shfl_up(incl, o);
-            if (lane >= o) incl += t;
+          for (int o = 32; o > 0; o >>= 1) {
+            const uint32_t t = __shfl_xor(maxc, o);
+            maxc = t > maxc ? t : maxc;
           }
-          const uint32_t excl = incl - cnt;
-          const uint32_t total = __shfl(incl, 63);
+          maxc = __builtin_amdgcn_readfirstlane(maxc);
+          const uint32_t total = __builtin_amdgcn_readfirstlane(
+              (uint32_t)wave_sum((uint64_t)cnt));
           for (uint32_t lb = 0; lb < total; lb += GLIST) {
-            if (excl < lb + GLIST && excl + cnt > lb) {
-              uint64_t ff = f;
-              uint32_t rank = excl;
-              while (ff) {
+            uint64_t ff = f;
+            uint32_t base = 0;
+            for (uint32_t kr = 0; kr < maxc; ++kr) {
+              const bool has = cnt > kr;
+              const uint64_t mk = __ballot(has);
+              if (has) {
+                const uint32_t pos = base + __builtin_amdgcn_mbcnt_hi(
+                                                (uint32_t)(mk >> 32),
+                                                __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
                 const int bit = __builtin_ctzll(ff);
                 ff &= ff - 1ull;
-                if (rank >= lb && rank < lb + GLIST) lst[wib][rank - lb] = (uint16_t)((lane << 6) | bit);
-                ++rank;
+                if (pos >= lb && pos < lb + GLIST) lst[wib][pos - lb] = (uint16_t)((lane << 6) | bit);
               }
+              base += (uint32_t)__popcll(mk);
             }
             wave_lds_sync();
             const uint32_t n = total - lb < (uint32_t)GLIST ? total - lb : (uint32_t)GLIST;
