@@ -586,8 +586,149 @@ __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st,
   const int k = K > 0 ? K : p.fanout;
   uint64_t c[STAT_N] = {0, 0, 0, 0, 0, 0, 0, 0};
 
+  // One (source v, neighbour chunk, row slice): f = this lane's frontier word, rv = lane j's
+  // receiver slot of connection nb + j (STORE_E only).
+  auto body = [&](int64_t v, int64_t rb, int64_t deg, int chunk, int sl, uint64_t f,
+                  uint32_t rv) {
+    const int nb = chunk * GCHUNK;
+    const int nn = (int)(deg - nb < GCHUNK ? deg - nb : GCHUNK);
+    const bool all = deg <= k;
+    const int w = sl * 64 + lane;
+    const bool valid = w < W;
+    const bool anyf = __ballot(f != 0ull) != 0ull;
+    if (!anyf && !STORE_E) return;
+    if (anyf && !all) {
+      for (int j = 0; j < nn; ++j) tbl[wib][j][lane] = 0ull;
+      // rank-major compaction: list = every word's 1st set bit, then every word's 2nd set
+      // bit, ... so a 64-entry batch covers ~64 distinct words (distinct LDS table columns ->
+      // few bank conflicts), while every lane still gets equal Philox work
+      const uint32_t cnt = (uint32_t)__popcll(f);
+      uint32_t maxc = cnt;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t t = __shfl_xor(maxc, o);
+        maxc = t > maxc ? t : maxc;
+      }
+      maxc = __builtin_amdgcn_readfirstlane(maxc);
+      const uint32_t total =
+          __builtin_amdgcn_readfirstlane((uint32_t)wave_sum((uint64_t)cnt));
+      for (uint32_t lb = 0; lb < total; lb += GLIST) {
+        uint64_t ff = f;
+        uint32_t base = 0;
+        for (uint32_t kr = 0; kr < maxc; ++kr) {
+          const bool has = cnt > kr;
+          const uint64_t mk = __ballot(has);
+          if (has) {
+            const uint32_t pos =
+                base + __builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32),
+                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
+            const int bit = __builtin_ctzll(ff);
+            ff &= ff - 1ull;
+            if (pos >= lb && pos < lb + GLIST) lst[wib][pos - lb] = (uint16_t)((lane << 6) | bit);
+          }
+          base += (uint32_t)__popcll(mk);
+        }
+        wave_lds_sync();
+        const uint32_t n = total - lb < (uint32_t)GLIST ? total - lb : (uint32_t)GLIST;
+        for (uint32_t i = lane; i < n; i += 64) {
+          const uint32_t e = lst[wib][i];
+          const uint32_t wl = e >> 6, bit = e & 63u;
+          const uint32_t mg = p.msg_base + (uint32_t)((sl * 64 + (int)wl) * 64) + bit;
+          if constexpr (K > 0) {
+            uint32_t pk[K];
+            gossip_picks_t<K>((uint32_t)p.round, (uint32_t)v, mg, (uint32_t)deg, p.gseed_lo,
+                              p.gseed_hi, pk);
+#pragma unroll
+            for (int q = 0; q < K; ++q) {
+              const uint32_t jj = pk[q] - (uint32_t)nb;
+              if (jj < (uint32_t)nn) atomicOr((unsigned long long*)&tbl[wib][jj][wl], 1ull << bit);
+            }
+          } else {
+            uint32_t pk[16];
+            gossip_picks((uint32_t)p.round, (uint32_t)v, mg, (uint32_t)deg, k, p.gseed_lo,
+                         p.gseed_hi, pk);
+            for (int q = 0; q < k; ++q) {
+              const uint32_t jj = pk[q] - (uint32_t)nb;
+              if (jj < (uint32_t)nn) atomicOr((unsigned long long*)&tbl[wib][jj][wl], 1ull << bit);
+            }
+          }
+        }
+        wave_lds_sync();
+      }
+    }
+    for (int j = 0; j < nn; ++j) {
+      const uint64_t x = all ? f : (anyf ? tbl[wib][j][lane] : 0ull);
+      const uint64_t bal = __ballot(x != 0ull);
+      if (STORE_E) {
+        bool dropped = false;
+        if (CHURN && bal)
+          dropped = churn_dropped((uint32_t)p.round, (uint32_t)v, (uint32_t)g.colidx[rb + nb + j],
+                                  p.churn_thr, p.cseed_lo, p.cseed_hi);
+        // receiver-major: the row lands in the RECEIVER's slot for this connection, so the
+        // pull streams its own contiguous slot range
+        const uint32_t dslot = (uint32_t)__builtin_amdgcn_readlane((int)rv, j);
+        if (valid) st.E[(int64_t)dslot * W + w] = dropped ? 0ull : x;
+        if (!dropped && lane == 0) c[ST_SCATTER] += (uint64_t)__popcll(bal);
+      } else {
+        if (!bal) continue;
+        const int32_t u = g.colidx[rb + nb + j];
+        if (CHURN && churn_dropped((uint32_t)p.round, (uint32_t)v, (uint32_t)u, p.churn_thr,
+                                   p.cseed_lo, p.cseed_hi))
+          continue;
+        if (x) atomicOr((unsigned long long*)&nx[(int64_t)u * W + w], (unsigned long long)x);
+        if (lane == 0) {
+          atomicOr(&Tn[u >> 5], 1u << (u & 31));
+          c[ST_SCATTER] += (uint64_t)__popcll(bal);
+        }
+      }
+    }
+  };
+
   for (int64_t task = (int64_t)blockIdx.x * WPB + wib; task < ntasks;
        task += (int64_t)gridDim.x * WPB) {
+    if (task < nwords && nslices == 1) {
+      // pipelined: row offsets of the 32 peers in one load; the next active peer's frontier
+      // word and receiver slots are in flight while the current one computes
+      uint32_t todo = st.A[cur][task];
+      if (!todo) continue;
+      const int64_t base = task << 5;
+      int64_t rp = 0;
+      if (lane <= 32 && base + lane <= V) rp = g.rowptr[base + lane];
+      auto pick_next = [&](uint32_t& t, int64_t& rb, int64_t& deg) -> int {
+        while (t) {
+          const int b = __builtin_ctz(t);
+          t &= t - 1u;
+          rb = readlane64(rp, b);
+          deg = readlane64(rp, b + 1) - rb;
+          if (deg <= GCHUNK) return b;  // wider sources: their chunk items
+        }
+        return -1;
+      };
+      int64_t rb1 = 0, deg1 = 0, rb2 = 0, deg2 = 0;
+      int b1 = pick_next(todo, rb1, deg1);
+      uint64_t f1 = 0;
+      uint32_t rv1 = 0;
+      if (b1 >= 0) {
+        if (lane < W) f1 = Fc[(base + b1) * W + lane];
+        if (STORE_E && lane < deg1) rv1 = g.rev[rb1 + lane];
+      }
+      while (b1 >= 0) {
+        const int b2 = pick_next(todo, rb2, deg2);
+        uint64_t f2 = 0;
+        uint32_t rv2 = 0;
+        if (b2 >= 0) {
+          if (lane < W) f2 = Fc[(base + b2) * W + lane];
+          if (STORE_E && lane < deg2) rv2 = g.rev[rb2 + lane];
+        }
+        body(base + b1, rb1, deg1, 0, 0, f1, rv1);
+        b1 = b2;
+        rb1 = rb2;
+        deg1 = deg2;
+        f1 = f2;
+        rv1 = rv2;
+      }
+      continue;
+    }
     uint32_t todo;
     int64_t base;
     int chunk;
@@ -610,103 +751,12 @@ __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st,
       if (task < nwords && deg > GCHUNK) continue;  // hub: handled by its chunk items
       const int nb = chunk * GCHUNK;
       const int nn = (int)(deg - nb < GCHUNK ? deg - nb : GCHUNK);
-      const bool all = deg <= k;
+      uint32_t rv = 0;
+      if (STORE_E && lane < nn) rv = g.rev[rb + nb + lane];
       for (int sl = 0; sl < nslices; ++sl) {
         const int w = sl * 64 + lane;
-        const bool valid = w < W;
-        const uint64_t f = valid ? Fc[v * W + w] : 0ull;
-        const bool anyf = __ballot(f != 0ull) != 0ull;
-        if (!anyf && !STORE_E) continue;
-        if (anyf && !all) {
-          for (int j = 0; j < nn; ++j) tbl[wib][j][lane] = 0ull;
-          // rank-major compaction: list = every word's 1st set bit, then every word's 2nd
-          // set bit, ... so a 64-entry batch covers ~64 distinct words (distinct LDS table
-          // columns -> few bank conflicts), while every lane still gets equal work
-          const uint32_t cnt = (uint32_t)__popcll(f);
-          uint32_t maxc = cnt;
-#pragma unroll
-          for (int o = 32; o > 0; o >>= 1) {
-            const uint32_t t = __shfl_xor(maxc, o);
-            maxc = t > maxc ? t : maxc;
-          }
-          maxc = __builtin_amdgcn_readfirstlane(maxc);
-          const uint32_t total = __builtin_amdgcn_readfirstlane(
-              (uint32_t)wave_sum((uint64_t)cnt));
-          for (uint32_t lb = 0; lb < total; lb += GLIST) {
-            uint64_t ff = f;
-            uint32_t base = 0;
-            for (uint32_t kr = 0; kr < maxc; ++kr) {
-              const bool has = cnt > kr;
-              const uint64_t mk = __ballot(has);
-              if (has) {
-                const uint32_t pos = base + __builtin_amdgcn_mbcnt_hi(
-                                                (uint32_t)(mk >> 32),
-                                                __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
-                const int bit = __builtin_ctzll(ff);
-                ff &= ff - 1ull;
-                if (pos >= lb && pos < lb + GLIST) lst[wib][pos - lb] = (uint16_t)((lane << 6) | bit);
-              }
-              base += (uint32_t)__popcll(mk);
-            }
-            wave_lds_sync();
-            const uint32_t n = total - lb < (uint32_t)GLIST ? total - lb : (uint32_t)GLIST;
-            for (uint32_t i = lane; i < n; i += 64) {
-              const uint32_t e = lst[wib][i];
-              const uint32_t wl = e >> 6, bit = e & 63u;
-              const uint32_t mg = p.msg_base + (uint32_t)((sl * 64 + (int)wl) * 64) + bit;
-              if constexpr (K > 0) {
-                uint32_t pk[K];
-                gossip_picks_t<K>((uint32_t)p.round, (uint32_t)v, mg, (uint32_t)deg, p.gseed_lo,
-                                  p.gseed_hi, pk);
-#pragma unroll
-                for (int q = 0; q < K; ++q) {
-                  const uint32_t jj = pk[q] - (uint32_t)nb;
-                  if (jj < (uint32_t)nn)
-                    atomicOr((unsigned long long*)&tbl[wib][jj][wl], 1ull << bit);
-                }
-              } else {
-                uint32_t pk[16];
-                gossip_picks((uint32_t)p.round, (uint32_t)v, mg, (uint32_t)deg, k, p.gseed_lo,
-                             p.gseed_hi, pk);
-                for (int q = 0; q < k; ++q) {
-                  const uint32_t jj = pk[q] - (uint32_t)nb;
-                  if (jj < (uint32_t)nn)
-                    atomicOr((unsigned long long*)&tbl[wib][jj][wl], 1ull << bit);
-                }
-              }
-            }
-            wave_lds_sync();
-          }
-        }
-        uint32_t rv = 0;  // receiver-side slots of this chunk's connections (lane j)
-        if (STORE_E && lane < nn) rv = g.rev[rb + nb + lane];
-        for (int j = 0; j < nn; ++j) {
-          const uint64_t x = all ? f : (anyf ? tbl[wib][j][lane] : 0ull);
-          const uint64_t bal = __ballot(x != 0ull);
-          if (STORE_E) {
-            bool dropped = false;
-            if (CHURN && bal)
-              dropped = churn_dropped((uint32_t)p.round, (uint32_t)v,
-                                      (uint32_t)g.colidx[rb + nb + j], p.churn_thr, p.cseed_lo,
-                                      p.cseed_hi);
-            // receiver-major: the row lands in the RECEIVER's slot for this connection, so
-            // the pull streams its own contiguous slot range
-            const uint32_t dslot = (uint32_t)__builtin_amdgcn_readlane((int)rv, j);
-            if (valid) st.E[(int64_t)dslot * W + w] = dropped ? 0ull : x;
-            if (!dropped && lane == 0) c[ST_SCATTER] += (uint64_t)__popcll(bal);
-          } else {
-            if (!bal) continue;
-            const int32_t u = g.colidx[rb + nb + j];
-            if (CHURN && churn_dropped((uint32_t)p.round, (uint32_t)v, (uint32_t)u, p.churn_thr,
-                                       p.cseed_lo, p.cseed_hi))
-              continue;
-            if (x) atomicOr((unsigned long long*)&nx[(int64_t)u * W + w], (unsigned long long)x);
-            if (lane == 0) {
-              atomicOr(&Tn[u >> 5], 1u << (u & 31));
-              c[ST_SCATTER] += (uint64_t)__popcll(bal);
-            }
-          }
-        }
+        const uint64_t f = w < W ? Fc[v * W + w] : 0ull;
+        body(v, rb, deg, chunk, sl, f, rv);
       }
     }
   }
