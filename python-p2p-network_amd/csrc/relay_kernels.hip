@@ -636,12 +636,18 @@ __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st,
           const uint32_t mg = p.msg_base + (uint32_t)((sl * 64 + (int)wl) * 64) + bit;
           if constexpr (K > 0) {
             uint32_t pk[K];
-            gossip_picks_t<K>((uint32_t)p.round, (uint32_t)v, mg, (uint32_t)deg, p.gseed_lo,
-                              p.gseed_hi, pk);
+            if (p.ablate & 1u) {
+#pragma unroll
+              for (int q = 0; q < K; ++q) pk[q] = (mg * 7u + (uint32_t)q) % (uint32_t)deg;
+            } else {
+              gossip_picks_t<K>((uint32_t)p.round, (uint32_t)v, mg, (uint32_t)deg, p.gseed_lo,
+                                p.gseed_hi, pk);
+            }
 #pragma unroll
             for (int q = 0; q < K; ++q) {
               const uint32_t jj = pk[q] - (uint32_t)nb;
-              if (jj < (uint32_t)nn) atomicOr((unsigned long long*)&tbl[wib][jj][wl], 1ull << bit);
+              if (jj < (uint32_t)nn && !(p.ablate & 4u))
+                atomicOr((unsigned long long*)&tbl[wib][jj][wl], 1ull << bit);
             }
           } else {
             uint32_t pk[16];
@@ -667,7 +673,7 @@ __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st,
         // receiver-major: the row lands in the RECEIVER's slot for this connection, so the
         // pull streams its own contiguous slot range
         const uint32_t dslot = (uint32_t)__builtin_amdgcn_readlane((int)rv, j);
-        if (valid) st.E[(int64_t)dslot * W + w] = dropped ? 0ull : x;
+        if (valid && !(p.ablate & 2u)) st.E[(int64_t)dslot * W + w] = dropped ? 0ull : x;
         if (!dropped && lane == 0) c[ST_SCATTER] += (uint64_t)__popcll(bal);
       } else {
         if (!bal) continue;

@@ -26,6 +26,8 @@ __device__ __forceinline__ u4 philox_b(u4 c, uint32_t k0, uint32_t k1) {
 }
 template <int V>
 __global__ void run(uint64_t n, uint32_t* out) {
+  extern __shared__ uint32_t pad[];
+  if (n == 0) pad[threadIdx.x] = 0;  // dynamic LDS only limits occupancy
   uint32_t acc = 0;
   uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x, nt = gridDim.x * (uint64_t)blockDim.x;
   for (uint64_t i = t; i < n; i += nt) {
@@ -39,9 +41,10 @@ int main() {
   uint32_t* out; CK(hipMalloc(&out, 64));
   hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
   uint64_t n = 1ull << 32;
-  for (int rep = 0; rep < 2; ++rep) {
-    for (int v = 0; v < 2; ++v) {
-      auto L = [&] { if (v == 0) run<0><<<256 * 16, 256>>>(n, out); else run<1><<<256 * 16, 256>>>(n, out); };
+  for (int lds : {0, 20 * 1024, 36 * 1024, 64 * 1024}) {
+    for (int v = 0; v < 1; ++v) {
+      printf("dynamic LDS %d B/block: ", lds);
+      auto L = [&] { run<0><<<256 * 16, 256, lds>>>(n, out); };
       L(); CK(hipDeviceSynchronize());
       CK(hipEventRecord(a)); L(); CK(hipEventRecord(b)); CK(hipEventSynchronize(b));
       float ms; CK(hipEventElapsedTime(&ms, a, b));
