@@ -56,6 +56,14 @@ __device__ __forceinline__ void flush_stats(unsigned long long* stats, const uin
   }
 }
 
+// Load through the constant address space: a wave-uniform address then becomes a scalar
+// load (s_load, counted on lgkmcnt) instead of a vector load whose vmcnt wait would also wait
+// for every row store the wave still has in flight.  Only for data no kernel writes.
+template <class T>
+__device__ __forceinline__ T ldc(const T* p) {
+  return *(const __attribute__((address_space(4))) T*)p;
+}
+
 // wave index inside the block, forced into an SGPR so task indices stay scalar
 __device__ __forceinline__ int wave_in_block() {
   return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -698,14 +706,15 @@ __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st,
       uint32_t todo = st.A[cur][task];
       if (!todo) continue;
       const int64_t base = task << 5;
-      int64_t rp = 0;
-      if (lane <= 32 && base + lane <= V) rp = g.rowptr[base + lane];
+      // row offsets by SCALAR loads (lgkmcnt): a vector load here would make every vertex
+      // wait on vmcnt, i.e. on the previous vertex's outstanding row stores
       auto pick_next = [&](uint32_t& t, int64_t& rb, int64_t& deg) -> int {
         while (t) {
           const int b = __builtin_ctz(t);
           t &= t - 1u;
-          rb = readlane64(rp, b);
-          deg = readlane64(rp, b + 1) - rb;
+          const int64_t vv = __builtin_amdgcn_readfirstlane((int)(base + b));
+          rb = ldc(g.rowptr + vv);
+          deg = ldc(g.rowptr + vv + 1) - rb;
           if (deg <= GCHUNK) return b;  // wider sources: their chunk items
         }
         return -1;
