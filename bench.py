@@ -41,28 +41,38 @@ WORKLOADS = {
 KCLASS = ("seed_update", "flood_pull", "gossip_scatter", "record")
 
 
-def model_bytes(rounds, mode):
-    """Algorithmic HBM bytes per kernel class for one run (DESIGN.md "byte model").
+def model_bytes(rounds, mode, W):
+    """Algorithmic HBM bytes per kernel class for one run.
 
     flood pull, round r:  8*wedges[r-1] + 8*words[r-1] + 4*degact[r-1]
                                         + 8*peers[r-1] + 24*words[r]
-    gossip update, round r:             24*touched[r] (next read+clear, seen read)
-                                        + 16*words[r] (seen write, frontier write)
     gossip scatter, round r:            8*words[r] + 8*peers[r] + 4*degact[r]
-                                        + 16*scatter[r] (read-modify-write of each pushed word)
+                                        + sparse form: 16*scatter[r] (read-modify-write of
+                                          each pushed word by a row atomicOr)
+                                        + dense form:  8*W*degact[r] (every connection row of
+                                          an active sender is stored whole)
+    gossip consume, round r >= 1:       after a sparse round: 24*touched[r] + 16*words[r]
+                                        after a dense round:  8*W*degact[r-1] + 24*words[r]
+    A round's push form is read off the next round: touched_words > 0 <=> row atomics.
     """
     b = {k: 0 for k in KCLASS}
+    n = len(rounds)
+    dense = [i + 1 < n and rounds[i + 1].touched_words == 0 and rounds[i].active_vertices > 0
+             for i in range(n)]
     for i, r in enumerate(rounds):
         if mode == "flood":
             if i >= 1:
                 p = rounds[i - 1]
                 b["flood_pull"] += (8 * p.wedges + 8 * p.active_words + 4 * p.deg_active
                                     + 8 * p.active_vertices + 24 * r.active_words)
-        else:
-            if i >= 1:
+            continue
+        if i >= 1:
+            if dense[i - 1]:
+                b["seed_update"] += 8 * W * rounds[i - 1].deg_active + 24 * r.active_words
+            else:
                 b["seed_update"] += 24 * r.touched_words + 16 * r.active_words
-            b["gossip_scatter"] += (8 * r.active_words + 8 * r.active_vertices + 4 * r.deg_active
-                                    + 16 * r.scatter_words)
+        b["gossip_scatter"] += (8 * r.active_words + 8 * r.active_vertices + 4 * r.deg_active
+                                + (8 * W * r.deg_active if dense[i] else 16 * r.scatter_words))
     return b
 
 
@@ -180,7 +190,7 @@ def main():
     del kt0
 
     last = all_rounds[-1]
-    mb = model_bytes(last, w["mode"])
+    mb = model_bytes(last, w["mode"], (M + 63) // 64)
     dominant = max(KCLASS, key=lambda k: kt[k][0])
     dom_ms, dom_n = kt[dominant]
     achieved = mb[dominant] / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
