@@ -38,7 +38,8 @@ WORKLOADS = {
                name="config2: 1k-peer random 8-regular, 64 flood broadcasts"),
 }
 
-KCLASS = ("seed_update", "flood_pull", "gossip_scatter", "record")
+KCLASS = ("seed", "flood_pull", "gossip_scatter_atomic", "record", "gossip_update", "gossip_pull",
+          "gossip_scatter_store", "reserved")
 
 
 def model_bytes(rounds, mode, W):
@@ -68,11 +69,14 @@ def model_bytes(rounds, mode, W):
             continue
         if i >= 1:
             if dense[i - 1]:
-                b["seed_update"] += 8 * W * rounds[i - 1].deg_active + 24 * r.active_words
+                b["gossip_pull"] += 8 * W * rounds[i - 1].deg_active + 24 * r.active_words
             else:
-                b["seed_update"] += 24 * r.touched_words + 16 * r.active_words
-        b["gossip_scatter"] += (8 * r.active_words + 8 * r.active_vertices + 4 * r.deg_active
-                                + (8 * W * r.deg_active if dense[i] else 16 * r.scatter_words))
+                b["gossip_update"] += 24 * r.touched_words + 16 * r.active_words
+        common = 8 * r.active_words + 8 * r.active_vertices + 4 * r.deg_active
+        if dense[i]:
+            b["gossip_scatter_store"] += common + 8 * W * r.deg_active
+        else:
+            b["gossip_scatter_atomic"] += common + 16 * r.scatter_words
     return b
 
 

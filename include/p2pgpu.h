@@ -114,9 +114,11 @@ int p2pg_get_new_deliveries(p2pg_engine* e, int64_t cap, int32_t* peer, int32_t*
  * P2PG_FLAG_RECORD (-1 = not delivered).  Any pointer may be NULL.                      */
 int p2pg_read_planes(p2pg_engine* e, uint64_t* seen, int32_t* hop, int32_t* parent);
 /* Summed device time per kernel class since the last reset (needs P2PG_FLAG_TIMING):
- * ms[0] seed/update, ms[1] flood pull, ms[2] gossip scatter, ms[3] record/other;
- * launches[i] likewise.                                                                 */
-int p2pg_kernel_times(p2pg_engine* e, double ms[4], int64_t launches[4]);
+ * 0 seed (origination), 1 flood pull, 2 gossip scatter by row atomics (sparse rounds),
+ * 3 record (validation), 4 gossip update (consume row atomics), 5 gossip pull (consume edge
+ * stores), 6 gossip scatter by edge stores (dense rounds), 7 reserved.                   */
+#define P2PG_KCLASS_N 8
+int p2pg_kernel_times(p2pg_engine* e, double ms[P2PG_KCLASS_N], int64_t launches[P2PG_KCLASS_N]);
 /* Launch on this hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); NULL =
  * the engine's own stream.                                                              */
 int p2pg_set_stream(p2pg_engine* e, void* hip_stream);

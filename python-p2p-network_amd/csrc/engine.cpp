@@ -60,8 +60,8 @@ struct p2pg_engine {
   // sync (no extra host synchronisation inside a round)
   std::vector<hipEvent_t> ev_pool;
   std::vector<int> ev_cls;  // class of pending pair i (events 2i, 2i+1)
-  double kms[4] = {0, 0, 0, 0};
-  int64_t klaunch[4] = {0, 0, 0, 0};
+  double kms[P2PG_KCLASS_N] = {0};
+  int64_t klaunch[P2PG_KCLASS_N] = {0};
   int32_t round = 0;
   bool done = false;
   bool have_state = false;
@@ -139,7 +139,7 @@ DevGraph graph(const p2pg_engine* e) {
   return DevGraph{e->d_rowptr, e->d_colidx, e->d_rev, e->d_H, e->V};
 }
 
-// Timed launch: kernel class cls in [0,4).
+// Timed launch: kernel class cls in [0, P2PG_KCLASS_N) (see include/p2pgpu.h).
 template <class F>
 int timed(p2pg_engine* e, int cls, F&& launch) {
   const bool timing = (e->cfg.flags & P2PG_FLAG_TIMING) != 0;
@@ -396,7 +396,7 @@ int p2pg_reset(p2pg_engine* e) {
   e->round = 0;
   e->done = false;
   e->last_push_e = false;
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < P2PG_KCLASS_N; ++i) {
     e->kms[i] = 0;
     e->klaunch[i] = 0;
   }
@@ -448,9 +448,9 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
     if ((rc = timed(e, 1, [&] { return launch_flood_pull(g, s, p, e->hp, e->stream); }))) return rc;
   } else if (e->last_push_e) {
     // previous round stored per-edge masks: gather them (pull, no atomics)
-    if ((rc = timed(e, 0, [&] { return launch_gossip_pull(g, s, p, e->hp, e->stream); }))) return rc;
+    if ((rc = timed(e, 5, [&] { return launch_gossip_pull(g, s, p, e->hp, e->stream); }))) return rc;
   } else {
-    if ((rc = timed(e, 0, [&] { return launch_gossip_update(g, s, p, e->stream); }))) return rc;
+    if ((rc = timed(e, 4, [&] { return launch_gossip_update(g, s, p, e->stream); }))) return rc;
   }
   if (s.hop)
     if ((rc = timed(e, 3, [&] { return launch_record(g, s, p, e->stream); }))) return rc;
@@ -487,7 +487,7 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
                 e->e_thresh * (double)tot[ST_ACTIVE_V] * (double)e->W && tot[ST_ACTIVE_V] > 0;
       }
     }
-    if ((rc = timed(e, 2, [&] {
+    if ((rc = timed(e, use_e ? 6 : 2, [&] {
            return launch_gossip_scatter(g, s, p, e->d_hub, e->n_hub, use_e, e->stream);
          })))
       return rc;
@@ -592,9 +592,9 @@ int p2pg_read_planes(p2pg_engine* e, uint64_t* seen, int32_t* hop, int32_t* pare
   return P2PG_OK;
 }
 
-int p2pg_kernel_times(p2pg_engine* e, double ms[4], int64_t launches[4]) {
+int p2pg_kernel_times(p2pg_engine* e, double ms[P2PG_KCLASS_N], int64_t launches[P2PG_KCLASS_N]) {
   if (!e) return P2PG_ERR_ARG;
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < P2PG_KCLASS_N; ++i) {
     if (ms) ms[i] = e->kms[i];
     if (launches) launches[i] = e->klaunch[i];
   }

@@ -236,13 +236,17 @@ class GraphNetwork:
         self._check(_lib.lib().p2pg_read_planes(self._h, None, _lib.ptr(hop), _lib.ptr(par)))
         return hop, par
 
+    KERNEL_CLASSES = ("seed", "flood_pull", "gossip_scatter_atomic", "record", "gossip_update",
+                      "gossip_pull", "gossip_scatter_store", "reserved")
+
     def kernel_times(self):
-        """Summed device ms and launch counts per kernel class (needs timing=True)."""
-        ms = np.zeros(4, dtype=np.float64)
-        n = np.zeros(4, dtype=np.int64)
-        self._check(_lib.lib().p2pg_kernel_times(self._h, _lib.ptr(ms), _lib.ptr(n)))
-        names = ("seed_update", "flood_pull", "gossip_scatter", "record")
-        return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(names)}
+        """Summed device ms and launch counts per kernel class since the last reset (needs
+        timing=True); classes as in include/p2pgpu.h (P2PG_KCLASS_N)."""
+        n = len(self.KERNEL_CLASSES)
+        ms = np.zeros(n, dtype=np.float64)
+        cnt = np.zeros(n, dtype=np.int64)
+        self._check(_lib.lib().p2pg_kernel_times(self._h, _lib.ptr(ms), _lib.ptr(cnt)))
+        return {k: (float(ms[i]), int(cnt[i])) for i, k in enumerate(self.KERNEL_CLASSES)}
 
     def device_philox(self, ctr, key):
         """Evaluate Philox4x32-10 on the GPU for counters [n, 4] (KAT hook)."""

@@ -47,13 +47,18 @@ def calib(d):
 
 
 def cls(name):
+    """rocprof kernel name -> bench.py timer class (include/p2pgpu.h P2PG_KCLASS_N)."""
+    tmpl = name.split("<", 1)[1].split(">(")[0] if "<" in name else ""
     if "k_gossip_scatter" in name:
-        return "gossip_scatter"
+        return "gossip_scatter_store" if tmpl.rstrip().endswith("true") else "gossip_scatter_atomic"
     if "k_pull" in name:
-        tmpl = name.split("k_pull")[1].split("(")[0]  # e.g. "1<false, true>"
-        return "gossip_pull" if tmpl.rstrip().endswith("true>") else "flood_pull"
-    if "k_gossip_update" in name or "k_seed" in name or "k_zero" in name:
-        return "seed_update"
+        return "gossip_pull" if tmpl.rstrip().endswith("true") else "flood_pull"
+    if "k_gossip_update" in name:
+        return "gossip_update"
+    if "k_seed" in name or "k_zero_rows" in name:
+        return "seed"
+    if "k_record" in name:
+        return "record"
     return None
 
 
@@ -70,7 +75,8 @@ def main():
         a = agg[k]
         a["fetch"] += c.get("FETCH_SIZE", 0.0) * 1024 * rf
         a["write"] += c.get("WRITE_SIZE", 0.0) * 1024 * wf
-        a["n"] += 1 if "FETCH_SIZE" in c else 0
+        # hub partial/finalize kernels ride in the same timed launch group as their k_pull1
+        a["n"] += 1 if ("FETCH_SIZE" in c and "k_pull_hub" not in name) else 0
         a["ns"] += c["ns"] if "FETCH_SIZE" in c else 0
     res = {"workload": wl, "calibration": cal, "source": run_dir, "kernels": {}}
     # the scatter and both consume kernels share class names with bench.py's timers
@@ -78,12 +84,6 @@ def main():
         n = max(a["n"], 1)
         res["kernels"][k] = {"launches": a["n"], "bytes_per_launch": (a["fetch"] + a["write"]) / n,
                              "read_bytes_per_launch": a["fetch"] / n, "write_bytes_per_launch": a["write"] / n}
-    if "gossip_pull" in res["kernels"] or "seed_update" in res["kernels"]:
-        # bench.py's "seed_update" timer class covers update + gossip pull launches
-        su = [res["kernels"][k] for k in ("seed_update", "gossip_pull") if k in res["kernels"]]
-        n = sum(x["launches"] for x in su)
-        tot = sum(x["bytes_per_launch"] * x["launches"] for x in su)
-        res["kernels"]["seed_update_combined"] = {"launches": n, "bytes_per_launch": tot / max(n, 1)}
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 
