@@ -48,6 +48,8 @@ extern "C" {
 
 #define P2PG_FLAG_RECORD 1u /* keep hop/parent planes [V][M] (validation scale)            */
 #define P2PG_FLAG_TIMING 2u /* per-kernel HIP-event timing (p2pg_kernel_times)              */
+#define P2PG_FLAG_NO_AUTOSTOP 4u /* partitioned runs: keep stepping after a locally quiet
+                                    round (the caller decides global quiescence)          */
 
 typedef struct p2pg_engine p2pg_engine;
 typedef struct p2pg_graph p2pg_graph;
@@ -119,6 +121,22 @@ int p2pg_read_planes(p2pg_engine* e, uint64_t* seen, int32_t* hop, int32_t* pare
  * stores), 6 gossip scatter by edge stores (dense rounds), 7 reserved.                   */
 #define P2PG_KCLASS_N 8
 int p2pg_kernel_times(p2pg_engine* e, double ms[P2PG_KCLASS_N], int64_t launches[P2PG_KCLASS_N]);
+/* ---- vertex-partitioned runs (one engine per GPU) ---------------------
+ * The caller loads the rank's LOCAL graph: owned peers plus ghost peers (remote neighbours),
+ * all numbered in ascending GLOBAL id order (so lowest-id tie-breaks are unchanged); ghosts
+ * have empty rows.  gid[local] = global id (Philox keys, reported ids).  send_local = owned
+ * boundary peers in the order the peers' ghost blocks expect them; recv_local = ghost peers
+ * in the order the owners send them.  After each p2pg_step the caller moves rows between
+ * ranks (e.g. RCCL all-to-all): plane 0 = frontier rows (pack from send_local, unpack into
+ * recv_local, before the next flood step); plane 1 = gossip pushes addressed to ghosts (pack
+ * from recv_local -- cleared locally --, unpack ORed into send_local).  Buffers are device
+ * memory of n x W uint64 words.  Replaces the cross-host TCP fan-out of
+ * NodeConnection.send (nodeconnection.py:107-160).                                      */
+int p2pg_set_global_ids(p2pg_engine* e, const int32_t* gid);
+int p2pg_set_exchange(p2pg_engine* e, int64_t n_send, const int32_t* send_local, int64_t n_recv,
+                      const int32_t* recv_local);
+int p2pg_exchange_pack(p2pg_engine* e, int32_t plane, void* dev_buf);
+int p2pg_exchange_unpack(p2pg_engine* e, int32_t plane, const void* dev_buf);
 /* Launch on this hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); NULL =
  * the engine's own stream.                                                              */
 int p2pg_set_stream(p2pg_engine* e, void* hip_stream);

@@ -45,6 +45,12 @@ struct p2pg_engine {
   int64_t* d_hub_begin = nullptr;
   uint64_t* d_partial = nullptr;
   HubPlan hp{};
+  // vertex-partitioned runs
+  int32_t* d_gid = nullptr;
+  std::vector<int32_t> h_gid;
+  int32_t* d_send = nullptr;
+  int32_t* d_recv = nullptr;
+  int64_t n_send = 0, n_recv = 0;
   bool last_push_e = false;    // gossip: pushes of the previous round went to E (dense)
   double e_thresh = 0.1;       // store-mode when active words >= thresh * active rows * W
   int push_mode = 0;           // 0 auto, 1 always row atomics, 2 always edge stores
@@ -116,6 +122,11 @@ void free_graph(p2pg_engine* e) {
   dfree(e->d_hubs);
   dfree(e->d_hub_begin);
   dfree(e->d_partial);
+  dfree(e->d_gid);
+  dfree(e->d_send);
+  dfree(e->d_recv);
+  e->h_gid.clear();
+  e->n_send = e->n_recv = 0;
   e->hp = HubPlan{};
   e->n_hub = 0;
 }
@@ -136,7 +147,7 @@ RoundParams params(const p2pg_engine* e) {
 }
 
 DevGraph graph(const p2pg_engine* e) {
-  return DevGraph{e->d_rowptr, e->d_colidx, e->d_rev, e->d_H, e->V};
+  return DevGraph{e->d_rowptr, e->d_colidx, e->d_rev, e->d_H, e->d_gid, e->V};
 }
 
 // Timed launch: kernel class cls in [0, P2PG_KCLASS_N) (see include/p2pgpu.h).
@@ -478,7 +489,7 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
     // push form for this round's sends: row atomics when the frontier is sparse, whole-row
     // edge-mask stores (+ pull next round) when most words of the active rows are set
     bool use_e = false;
-    if (s.E) {
+    if (s.E && !e->d_gid) {  // partitioned gossip pushes by row atomics (ghost rows travel)
       if (e->push_mode == 2) {
         use_e = true;
       } else if (e->push_mode == 0) {
@@ -508,7 +519,7 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
     out->touched_words = tot[ST_AUX];
   }
   e->round += 1;
-  if (!active) e->done = true;
+  if (!active && !(e->cfg.flags & P2PG_FLAG_NO_AUTOSTOP)) e->done = true;
   return active ? 1 : 0;
 }
 
@@ -569,11 +580,13 @@ int p2pg_get_new_deliveries(p2pg_engine* e, int64_t cap, int32_t* peer, int32_t*
   std::sort(idx.begin(), idx.end(), [&](int64_t a, int64_t b) {
     return hp[a] != hp[b] ? hp[a] < hp[b] : hm[a] < hm[b];
   });
+  const bool map = !e->h_gid.empty();
   for (int64_t i = 0; i < n; ++i) {
-    peer[i] = hp[idx[i]];
+    const int32_t pr = hpar[idx[i]];
+    peer[i] = map ? e->h_gid[hp[idx[i]]] : hp[idx[i]];
     msg[i] = hm[idx[i]];
     hop[i] = p.round;
-    parent[i] = hpar[idx[i]];
+    parent[i] = (map && pr >= 0) ? e->h_gid[pr] : pr;
   }
   *n_out = (int64_t)cnt;
   return P2PG_OK;
@@ -588,8 +601,75 @@ int p2pg_read_planes(p2pg_engine* e, uint64_t* seen, int32_t* hop, int32_t* pare
   if (seen) HIPCHK(e, hipMemcpy(seen, e->st.seen, e->plane_bytes, hipMemcpyDeviceToHost));
   const size_t hb = (size_t)e->V * e->M * sizeof(int32_t);
   if (hop) HIPCHK(e, hipMemcpy(hop, e->st.hop, hb, hipMemcpyDeviceToHost));
-  if (parent) HIPCHK(e, hipMemcpy(parent, e->st.parent, hb, hipMemcpyDeviceToHost));
+  if (parent) {
+    HIPCHK(e, hipMemcpy(parent, e->st.parent, hb, hipMemcpyDeviceToHost));
+    if (!e->h_gid.empty())  // local -> global sender ids
+      for (size_t i = 0; i < (size_t)e->V * e->M; ++i)
+        if (parent[i] >= 0) parent[i] = e->h_gid[parent[i]];
+  }
   return P2PG_OK;
+}
+
+int p2pg_set_global_ids(p2pg_engine* e, const int32_t* gid) {
+  if (!e || !e->d_rowptr) return fail(e, P2PG_ERR_STATE, "set_global_ids: load a graph first");
+  HIPCHK(e, hipSetDevice(e->cfg.device));
+  dfree(e->d_gid);
+  e->h_gid.clear();
+  if (!gid) return P2PG_OK;
+  for (int64_t v = 1; v < e->V; ++v)
+    if (gid[v] <= gid[v - 1])
+      return fail(e, P2PG_ERR_ARG, "set_global_ids: ids must be strictly ascending (global order)");
+  e->h_gid.assign(gid, gid + e->V);
+  HIPCHK(e, hipMalloc((void**)&e->d_gid, sizeof(int32_t) * e->V));
+  HIPCHK(e, hipMemcpy(e->d_gid, gid, sizeof(int32_t) * e->V, hipMemcpyHostToDevice));
+  return P2PG_OK;
+}
+
+int p2pg_set_exchange(p2pg_engine* e, int64_t n_send, const int32_t* send_local, int64_t n_recv,
+                      const int32_t* recv_local) {
+  if (!e || !e->d_rowptr || n_send < 0 || n_recv < 0 || (n_send && !send_local) ||
+      (n_recv && !recv_local))
+    return fail(e, P2PG_ERR_ARG, "set_exchange: bad arguments");
+  for (int64_t i = 0; i < n_send; ++i)
+    if (send_local[i] < 0 || send_local[i] >= e->V) return fail(e, P2PG_ERR_ARG, "set_exchange: send id out of range");
+  for (int64_t i = 0; i < n_recv; ++i)
+    if (recv_local[i] < 0 || recv_local[i] >= e->V) return fail(e, P2PG_ERR_ARG, "set_exchange: recv id out of range");
+  HIPCHK(e, hipSetDevice(e->cfg.device));
+  dfree(e->d_send);
+  dfree(e->d_recv);
+  e->n_send = n_send;
+  e->n_recv = n_recv;
+  HIPCHK(e, hipMalloc((void**)&e->d_send, sizeof(int32_t) * (n_send ? n_send : 1)));
+  HIPCHK(e, hipMalloc((void**)&e->d_recv, sizeof(int32_t) * (n_recv ? n_recv : 1)));
+  if (n_send) HIPCHK(e, hipMemcpy(e->d_send, send_local, sizeof(int32_t) * n_send, hipMemcpyHostToDevice));
+  if (n_recv) HIPCHK(e, hipMemcpy(e->d_recv, recv_local, sizeof(int32_t) * n_recv, hipMemcpyHostToDevice));
+  return P2PG_OK;
+}
+
+static int exchange(p2pg_engine* e, int32_t plane, bool pack, void* buf) {
+  if (!e || !e->have_state || e->round == 0 || (plane != 0 && plane != 1))
+    return fail(e, P2PG_ERR_STATE, "exchange: need a completed round and plane 0 or 1");
+  if (plane == 1 && e->cfg.mode != P2PG_MODE_GOSSIP)
+    return fail(e, P2PG_ERR_ARG, "exchange: plane 1 is for gossip pushes");
+  HIPCHK(e, hipSetDevice(e->cfg.device));
+  const int r = e->round - 1;  // the round step() completed
+  // plane 0 moves frontier rows owner -> ghost; plane 1 moves pushed rows ghost -> owner
+  const bool use_send_list = (plane == 0) == pack;
+  const int32_t* ids = use_send_list ? e->d_send : e->d_recv;
+  const int64_t n = use_send_list ? e->n_send : e->n_recv;
+  hipError_t rr = pack ? launch_pack(e->st, plane, r, ids, n, (uint64_t*)buf, e->stream)
+                       : launch_unpack(e->st, plane, r, ids, n, (const uint64_t*)buf, e->stream);
+  if (rr == hipSuccess) rr = hipStreamSynchronize(e->stream);
+  if (rr != hipSuccess) return fail(e, P2PG_ERR_HIP, std::string("exchange: ") + hipGetErrorString(rr));
+  return P2PG_OK;
+}
+
+int p2pg_exchange_pack(p2pg_engine* e, int32_t plane, void* dev_buf) {
+  return exchange(e, plane, true, dev_buf);
+}
+
+int p2pg_exchange_unpack(p2pg_engine* e, int32_t plane, const void* dev_buf) {
+  return exchange(e, plane, false, const_cast<void*>(dev_buf));
 }
 
 int p2pg_kernel_times(p2pg_engine* e, double ms[P2PG_KCLASS_N], int64_t launches[P2PG_KCLASS_N]) {

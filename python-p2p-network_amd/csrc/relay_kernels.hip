@@ -64,6 +64,12 @@ __device__ __forceinline__ T ldc(const T* p) {
   return *(const __attribute__((address_space(4))) T*)p;
 }
 
+// Global peer id of a local vertex (partitioned runs keep ghosts in global-id order; the
+// Philox keys of churn and gossip are global ids so partitioning cannot change results).
+__device__ __forceinline__ uint32_t gidx(const DevGraph& g, int64_t x) {
+  return g.gid ? (uint32_t)g.gid[x] : (uint32_t)x;
+}
+
 // wave index inside the block, forced into an SGPR so task indices stay scalar
 __device__ __forceinline__ int wave_in_block() {
   return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -148,7 +154,7 @@ __global__ __launch_bounds__(256) void k_pull(DevGraph g, DevState st, RoundPara
               const int32_t v = g.colidx[j];
               act = bit_test(Ap, v);
               if (CHURN && act)
-                act = !churn_dropped((uint32_t)(p.round - 1), (uint32_t)u, (uint32_t)v,
+                act = !churn_dropped((uint32_t)(p.round - 1), gidx(g, u), gidx(g, v),
                                      p.churn_thr, p.cseed_lo, p.cseed_hi);
               srow = GOSSIP ? (uint32_t)j : (uint32_t)v;
             }
@@ -282,7 +288,7 @@ __global__ __launch_bounds__(256) void k_pull1(DevGraph g, DevState st, RoundPar
       if (j < q.end) {
         a = bit_test(Ap, q.v);
         if (CHURN && a)
-          a = !churn_dropped((uint32_t)(p.round - 1), (uint32_t)(u0 + q.b), (uint32_t)q.v,
+          a = !churn_dropped((uint32_t)(p.round - 1), gidx(g, u0 + q.b), gidx(g, q.v),
                              p.churn_thr, p.cseed_lo, p.cseed_hi);
       }
       q.act = a;
@@ -343,7 +349,7 @@ __global__ __launch_bounds__(256) void k_pull1(DevGraph g, DevState st, RoundPar
             srow = GOSSIP ? (uint32_t)j : (uint32_t)v;
             a = bit_test(Ap, v);
             if (CHURN && a)
-              a = !churn_dropped((uint32_t)(p.round - 1), (uint32_t)u, (uint32_t)v, p.churn_thr,
+              a = !churn_dropped((uint32_t)(p.round - 1), gidx(g, u), gidx(g, v), p.churn_thr,
                                  p.cseed_lo, p.cseed_hi);
           }
           m = __ballot(a);
@@ -414,7 +420,7 @@ __global__ __launch_bounds__(256) void k_pull_hub_partial(DevGraph g, DevState s
           srow = GOSSIP ? (uint32_t)j : (uint32_t)v;
           a = bit_test(Ap, v);
           if (CHURN && a)
-            a = !churn_dropped((uint32_t)(p.round - 1), (uint32_t)u, (uint32_t)v, p.churn_thr,
+            a = !churn_dropped((uint32_t)(p.round - 1), gidx(g, u), gidx(g, v), p.churn_thr,
                                p.cseed_lo, p.cseed_hi);
         }
         uint64_t m = __ballot(a);
@@ -648,7 +654,7 @@ __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st,
 #pragma unroll
               for (int q = 0; q < K; ++q) pk[q] = (mg * 7u + (uint32_t)q) % (uint32_t)deg;
             } else {
-              gossip_picks_t<K>((uint32_t)p.round, (uint32_t)v, mg, (uint32_t)deg, p.gseed_lo,
+              gossip_picks_t<K>((uint32_t)p.round, gidx(g, v), mg, (uint32_t)deg, p.gseed_lo,
                                 p.gseed_hi, pk);
             }
 #pragma unroll
@@ -659,7 +665,7 @@ __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st,
             }
           } else {
             uint32_t pk[16];
-            gossip_picks((uint32_t)p.round, (uint32_t)v, mg, (uint32_t)deg, k, p.gseed_lo,
+            gossip_picks((uint32_t)p.round, gidx(g, v), mg, (uint32_t)deg, k, p.gseed_lo,
                          p.gseed_hi, pk);
             for (int q = 0; q < k; ++q) {
               const uint32_t jj = pk[q] - (uint32_t)nb;
@@ -676,7 +682,7 @@ __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st,
       if (STORE_E) {
         bool dropped = false;
         if (CHURN && bal)
-          dropped = churn_dropped((uint32_t)p.round, (uint32_t)v, (uint32_t)g.colidx[rb + nb + j],
+          dropped = churn_dropped((uint32_t)p.round, gidx(g, v), gidx(g, g.colidx[rb + nb + j]),
                                   p.churn_thr, p.cseed_lo, p.cseed_hi);
         // receiver-major: the row lands in the RECEIVER's slot for this connection, so the
         // pull streams its own contiguous slot range
@@ -686,7 +692,7 @@ __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st,
       } else {
         if (!bal) continue;
         const int32_t u = g.colidx[rb + nb + j];
-        if (CHURN && churn_dropped((uint32_t)p.round, (uint32_t)v, (uint32_t)u, p.churn_thr,
+        if (CHURN && churn_dropped((uint32_t)p.round, gidx(g, v), gidx(g, u), p.churn_thr,
                                    p.cseed_lo, p.cseed_hi))
           continue;
         if (x) atomicOr((unsigned long long*)&nx[(int64_t)u * W + w], (unsigned long long)x);
@@ -793,7 +799,7 @@ __device__ int32_t find_parent(const DevGraph& g, const DevState& st, const Roun
     const int32_t v = g.colidx[e];
     if (!bit_test(st.A[prv], v)) continue;
     if (!(st.F[prv][(int64_t)v * W + w] & bit)) continue;
-    if (p.churn_thr && churn_dropped((uint32_t)(p.round - 1), (uint32_t)u, (uint32_t)v,
+    if (p.churn_thr && churn_dropped((uint32_t)(p.round - 1), gidx(g, u), gidx(g, v),
                                      p.churn_thr, p.cseed_lo, p.cseed_hi))
       continue;
     if (p.mode == 1) {
@@ -806,7 +812,7 @@ __device__ int32_t find_parent(const DevGraph& g, const DevState& st, const Roun
           if (g.colidx[vb + mid] < u) lo = mid + 1; else hi = mid;
         }
         uint32_t pk[16];
-        gossip_picks((uint32_t)(p.round - 1), (uint32_t)v, p.msg_base + (uint32_t)m,
+        gossip_picks((uint32_t)(p.round - 1), gidx(g, v), p.msg_base + (uint32_t)m,
                      (uint32_t)dv, p.fanout, p.gseed_lo, p.gseed_hi, pk);
         bool hit = false;
         for (int q = 0; q < p.fanout; ++q) hit |= (pk[q] == (uint32_t)lo);
@@ -879,6 +885,54 @@ __global__ __launch_bounds__(256) void k_deliveries(DevGraph g, DevState st, Rou
           }
         }
       }
+    }
+  }
+}
+
+// Vertex-partitioned runs.  plane 0: boundary frontier rows of round `round` out (inactive
+// rows as zeros) / ghost frontier rows in (+ A bits).  plane 1 (gossip): pushes pending for
+// round `round`+1 into ghost rows out (cleared locally with their T bits) / ORed into the
+// owner's rows in (+ T bits).  One wave per row, lane = word.
+__global__ __launch_bounds__(256) void k_pack(DevState st, int plane, int round,
+                                              const int32_t* __restrict__ ids, int64_t n,
+                                              uint64_t* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int W = st.W;
+  const int64_t nw = (int64_t)gridDim.x * WPB;
+  for (int64_t i = (int64_t)blockIdx.x * WPB + wave_in_block(); i < n; i += nw) {
+    const int64_t v = ids[i];
+    if (plane == 0) {
+      const bool act = bit_test(st.A[round & 1], v);
+      for (int w = lane; w < W; w += 64) out[i * W + w] = act ? st.F[round & 1][v * W + w] : 0ull;
+    } else {
+      uint64_t* nx = st.next[(round + 1) & 1];
+      for (int w = lane; w < W; w += 64) {
+        out[i * W + w] = nx[v * W + w];
+        nx[v * W + w] = 0ull;
+      }
+      if (lane == 0) atomicAnd(&st.T[(round + 1) & 1][v >> 5], ~(1u << (v & 31)));
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_unpack(DevState st, int plane, int round,
+                                                const int32_t* __restrict__ ids, int64_t n,
+                                                const uint64_t* __restrict__ in) {
+  const int lane = threadIdx.x & 63;
+  const int W = st.W;
+  const int64_t nw = (int64_t)gridDim.x * WPB;
+  for (int64_t i = (int64_t)blockIdx.x * WPB + wave_in_block(); i < n; i += nw) {
+    const int64_t v = ids[i];
+    bool any = false;
+    for (int w = lane; w < W; w += 64) {
+      const uint64_t x = in[i * W + w];
+      any |= x != 0ull;
+      if (plane == 0) st.F[round & 1][v * W + w] = x;
+      else if (x) atomicOr((unsigned long long*)&st.next[(round + 1) & 1][v * W + w], (unsigned long long)x);
+    }
+    if (__ballot(any) && lane == 0) {
+      if (plane == 0) atomicOr(&st.A[round & 1][v >> 5], 1u << (v & 31));
+      else atomicOr(&st.T[(round + 1) & 1][v >> 5], 1u << (v & 31));
     }
   }
 }
@@ -996,6 +1050,20 @@ hipError_t launch_deliveries(const DevGraph& g, const DevState& st, const RoundP
   const int grid = grid_tasks((g.V + 31) >> 5);
   hipLaunchKernelGGL(k_deliveries, dim3(grid), dim3(256), 0, s, g, st, p, cap, peer, msg,
                      parent, counter);
+  return hipGetLastError();
+}
+
+hipError_t launch_pack(const DevState& st, int plane, int round, const int32_t* ids, int64_t n,
+                       uint64_t* out, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_pack, dim3(grid_tasks(n)), dim3(256), 0, s, st, plane, round, ids, n, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_unpack(const DevState& st, int plane, int round, const int32_t* ids, int64_t n,
+                         const uint64_t* in, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_unpack, dim3(grid_tasks(n)), dim3(256), 0, s, st, plane, round, ids, n, in);
   return hipGetLastError();
 }
 

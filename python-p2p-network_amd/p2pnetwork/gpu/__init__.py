@@ -11,6 +11,7 @@ The HIP engine is reached through ctypes (``_lib``); there is no CPU fallback.
 from ._lib import P2PGError, LIB_PATH
 from .graph import PeerGraph, make_sources
 from .network import GraphNetwork, RoundStats, Deliveries, churn_threshold
+from .partition import VertexPartition, PartitionedNetwork, TorchTransport
 
 __all__ = ["P2PGError", "LIB_PATH", "PeerGraph", "make_sources", "GraphNetwork", "RoundStats",
-           "Deliveries", "churn_threshold"]
+           "Deliveries", "churn_threshold", "VertexPartition", "PartitionedNetwork", "TorchTransport"]

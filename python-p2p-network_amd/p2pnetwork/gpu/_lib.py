@@ -16,6 +16,7 @@ MODE_FLOOD = 0
 MODE_GOSSIP = 1
 FLAG_RECORD = 1
 FLAG_TIMING = 2
+FLAG_NO_AUTOSTOP = 4
 
 # graph kinds of p2pg_graph_generate
 GRAPH_RANDOM_REGULAR = 0
@@ -83,6 +84,10 @@ SIGNATURES = {
     "p2pg_get_new_deliveries": (ctypes.c_int, [_P, _I64, _P, _P, _P, _P, ctypes.POINTER(_I64)]),
     "p2pg_read_planes": (ctypes.c_int, [_P, _P, _P, _P]),
     "p2pg_kernel_times": (ctypes.c_int, [_P, _P, _P]),
+    "p2pg_set_global_ids": (ctypes.c_int, [_P, _P]),
+    "p2pg_set_exchange": (ctypes.c_int, [_P, _I64, _P, _I64, _P]),
+    "p2pg_exchange_pack": (ctypes.c_int, [_P, _I32, _P]),
+    "p2pg_exchange_unpack": (ctypes.c_int, [_P, _I32, _P]),
     "p2pg_set_stream": (ctypes.c_int, [_P, _P]),
     "p2pg_device_philox": (ctypes.c_int, [_P, _I32, _P, _P, _P]),
     "p2pg_last_error": (ctypes.c_char_p, [_P]),

@@ -75,7 +75,7 @@ class GraphNetwork:
 
     def __init__(self, graph, mode="flood", fanout=3, gossip_seed=0x5EED, churn=0.0,
                  churn_threshold_value=None, churn_seed=0xC0FFEE, record=False, timing=False,
-                 device=0, msg_id_base=0, callback=None):
+                 device=0, msg_id_base=0, callback=None, autostop=True):
         if not isinstance(graph, PeerGraph):
             raise TypeError("graph must be a PeerGraph")
         if mode not in ("flood", "gossip"):
@@ -93,7 +93,8 @@ class GraphNetwork:
         cfg.churn_threshold = int(churn_threshold_value if churn_threshold_value is not None
                                   else churn_threshold(churn))
         cfg.msg_id_base = int(msg_id_base)
-        cfg.flags = (_lib.FLAG_RECORD if record else 0) | (_lib.FLAG_TIMING if timing else 0)
+        cfg.flags = ((_lib.FLAG_RECORD if record else 0) | (_lib.FLAG_TIMING if timing else 0)
+                     | (0 if autostop else _lib.FLAG_NO_AUTOSTOP))
         cfg.device = int(device)
         self.config = cfg
         L = _lib.lib()
@@ -247,6 +248,27 @@ class GraphNetwork:
         cnt = np.zeros(n, dtype=np.int64)
         self._check(_lib.lib().p2pg_kernel_times(self._h, _lib.ptr(ms), _lib.ptr(cnt)))
         return {k: (float(ms[i]), int(cnt[i])) for i, k in enumerate(self.KERNEL_CLASSES)}
+
+    # -- vertex-partitioned runs (p2pnetwork.gpu.partition) --------------------------------
+    def set_global_ids(self, gid):
+        self._gid = np.ascontiguousarray(gid, dtype=np.int32)
+        self._check(_lib.lib().p2pg_set_global_ids(self._h, _lib.ptr(self._gid)))
+
+    def set_exchange(self, send_local, recv_local):
+        s = np.ascontiguousarray(send_local, dtype=np.int32)
+        r = np.ascontiguousarray(recv_local, dtype=np.int32)
+        self._check(_lib.lib().p2pg_set_exchange(self._h, len(s), _lib.ptr(s), len(r), _lib.ptr(r)))
+
+    def alloc_exchange(self, n_words):
+        """Device buffer for exchange rows (a torch tensor on this engine's GPU)."""
+        import torch
+        return torch.empty(max(int(n_words), 1), dtype=torch.int64, device=f"cuda:{self.config.device}")
+
+    def exchange_pack(self, plane, buf):
+        self._check(_lib.lib().p2pg_exchange_pack(self._h, int(plane), ctypes.c_void_p(buf.data_ptr())))
+
+    def exchange_unpack(self, plane, buf):
+        self._check(_lib.lib().p2pg_exchange_unpack(self._h, int(plane), ctypes.c_void_p(buf.data_ptr())))
 
     def device_philox(self, ctr, key):
         """Evaluate Philox4x32-10 on the GPU for counters [n, 4] (KAT hook)."""

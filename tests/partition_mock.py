@@ -1,0 +1,161 @@
+"""Test-only NumPy stand-in for one rank's engine in a vertex-partitioned run (CPU tests of
+p2pnetwork.gpu.partition with the gloo backend).  It restates, on the rank-local graph with
+ghost rows, exactly the contract of the C-ABI's partition entry points (include/p2pgpu.h):
+frontier rows valid only with their A bit, ghost rows filled by unpack, pushes to ghosts moved
+by pack/unpack, Philox keys on global ids.  Uses the oracle's Philox (tests may)."""
+import numpy as np
+
+from oracle import philox
+from p2pnetwork.gpu.network import RoundStats
+
+
+def _words(b):
+    """bool [n, M] -> uint64 [n, W]"""
+    n, M = b.shape
+    W = (M + 63) // 64
+    pad = np.zeros((n, W * 64), dtype=bool)
+    pad[:, :M] = b
+    return np.packbits(pad.reshape(n, W, 64), axis=2, bitorder="little").reshape(n, W * 8).view(np.uint64)
+
+
+def _bits(w, M):
+    n = w.shape[0]
+    if n == 0:
+        return np.zeros((0, M), dtype=bool)
+    return np.unpackbits(w.view(np.uint8).reshape(n, -1), axis=1, bitorder="little")[:, :M].astype(bool)
+
+
+class MockEngine:
+    def __init__(self, graph, mode="flood", fanout=3, gossip_seed=0, churn_threshold_value=0,
+                 churn_seed=0, record=False, timing=False, device=0, autostop=True):
+        self.g, self.mode, self.k = graph, mode, fanout
+        self.gseed, self.thr, self.cseed = gossip_seed, churn_threshold_value, churn_seed
+        self.V = graph.V
+        self.deg = graph.degree()
+        self.rows = np.repeat(np.arange(self.V), self.deg)
+        self.gid = np.arange(self.V)
+
+    def set_global_ids(self, gid):
+        self.gid = np.asarray(gid, dtype=np.int64)
+
+    def set_exchange(self, send_local, recv_local):
+        self.send, self.recv = np.asarray(send_local), np.asarray(recv_local)
+
+    def alloc_exchange(self, n_words):
+        import torch
+        return torch.zeros(max(int(n_words), 1), dtype=torch.int64)
+
+    def broadcast(self, src):
+        self.src = np.asarray(src, dtype=np.int64)
+        self.M = len(self.src)
+        self.reset()
+
+    def reset(self):
+        V, M = self.V, self.M
+        self.seen = np.zeros((V, M), bool)
+        self.F = np.zeros((V, M), bool)
+        self.next = np.zeros((V, M), bool)
+        self.cand = np.full((V, M), np.iinfo(np.int64).max)
+        self.hop = np.full((V, M), -1, np.int32)
+        self.par = np.full((V, M), -1, np.int32)
+        self.round = 0
+
+    def _stats(self, new, per_bit, scatter=0):
+        W = (self.M + 63) // 64
+        words = _words(new) != 0
+        pv = new.sum(1)
+        act = pv > 0
+        return RoundStats(self.round, int(pv.sum() > 0), int(pv.sum()), int((pv * per_bit).sum()),
+                          int(act.sum()), int(words.sum()), int((words.sum(1) * self.deg).sum()),
+                          int(self.deg[act].sum()), int(scatter), 0)
+
+    def _scatter(self):
+        """pushes of the current frontier into self.next (gossip)"""
+        vs, ms = np.nonzero(self.F)
+        keys = set()
+        for v, m in zip(vs, ms):
+            d = self.deg[v]
+            if d == 0:
+                continue
+            nb = self.g.colidx[self.g.rowptr[v]:self.g.rowptr[v + 1]]
+            if d <= self.k:
+                tg = nb
+            else:
+                pk = philox.gossip_picks(self.round, self.gid[v], m, d, self.k, self.gseed)[0]
+                tg = nb[pk]
+            for t in tg:
+                if philox.churn_dropped(self.round, self.gid[v], self.gid[t], self.thr, self.cseed):
+                    continue
+                self.next[t, m] = True
+                self.cand[t, m] = min(self.cand[t, m], self.gid[v])
+                keys.add((v, t, m // 64))
+        return len(keys)
+
+    def step(self):
+        V, M = self.V, self.M
+        if self.round == 0:
+            new = np.zeros((V, M), bool)
+            new[self.src, np.arange(M)] = True
+            self.seen |= new
+            self.F = new
+            self.hop[new] = 0
+        elif self.mode == "flood":
+            alive = ~philox.churn_dropped(self.round - 1, self.gid[self.rows], self.gid[self.g.colidx],
+                                          self.thr, self.cseed)
+            contrib = self.F[self.g.colidx] & alive[:, None]
+            arr = np.zeros((V, M), bool)
+            np.logical_or.at(arr, self.rows, contrib)
+            new = arr & ~self.seen
+            pend = new.copy()
+            for e in range(len(self.rows)):  # ascending slots = ascending global ids per row
+                u = self.rows[e]
+                hit = contrib[e] & pend[u]
+                if hit.any():
+                    self.par[u, hit] = self.gid[self.g.colidx[e]]
+                    pend[u] &= ~hit
+            self.seen |= new
+            self.hop[new] = self.round
+            self.F = new
+        else:
+            new = self.next & ~self.seen
+            self.par[new] = self.cand[new]
+            self.cand[self.next] = np.iinfo(np.int64).max
+            self.next[:] = False
+            self.seen |= new
+            self.hop[new] = self.round
+            self.F = new
+        per_bit = np.minimum(self.deg, self.k) if self.mode == "gossip" else np.maximum(self.deg - 1, 0)
+        st = self._stats(new, per_bit)
+        if self.mode == "gossip":
+            st.scatter_words = self._scatter()
+        self.round += 1
+        return st
+
+    def exchange_pack(self, plane, buf):
+        if plane == 0:
+            rows = self.F[self.send]
+        else:
+            rows = self.next[self.recv]
+            self.next[self.recv] = False
+        w = _words(rows).astype(np.int64).ravel()
+        buf[:len(w)] = __import__("torch").from_numpy(w)
+
+    def exchange_unpack(self, plane, buf):
+        arr = buf.cpu().numpy().astype(np.int64).view(np.uint64)
+        W = (self.M + 63) // 64
+        if plane == 0:
+            self.F[self.recv] = _bits(arr[:len(self.recv) * W].reshape(-1, W), self.M)
+        else:
+            b = _bits(arr[:len(self.send) * W].reshape(-1, W), self.M)
+            # a boundary peer appears once per neighbouring rank: OR, never overwrite
+            # (the device unpack uses atomicOr); gossip parents are not checked when partitioned
+            np.logical_or.at(self.next, self.send, b)
+
+    def seen_plane(self):
+        return _words(self.seen)
+
+    def hop_parent(self):
+        return self.hop, self.par
+
+    def close(self):
+        pass

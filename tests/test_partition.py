@@ -1,0 +1,117 @@
+"""Vertex-partitioned multi-GPU path (p2pnetwork.gpu.partition), exercised on CPU with the
+gloo backend (world size 2 and 3) through the real orchestration code; each rank's engine is
+the test-only NumPy stand-in of tests/partition_mock.py.  The union of the ranks' owned
+results must equal the single-graph oracle bit for bit (hop, parent, per-round counters)."""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+
+from conftest import trim_zeros
+from oracle import relay_oracle
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def make_graph(kind):
+    from p2pnetwork.gpu import PeerGraph
+    if kind == "ws":
+        return PeerGraph.watts_strogatz(240, 6, 0.2, seed=4)
+    if kind == "ba":
+        return PeerGraph.barabasi_albert(200, 3, seed=5)
+    edges = [(0, 1), (1, 2), (5, 6), (8, 9)]  # sparse: isolated peers, tiny components
+    return PeerGraph.from_edges(30, edges)
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4])
+@pytest.mark.parametrize("kind", ["ws", "ba", "sparse"])
+def test_partition_lists_are_symmetric_and_cover(world, kind):
+    from p2pnetwork.gpu import VertexPartition
+    g = make_graph(kind)
+    parts = [VertexPartition(g, world, r) for r in range(world)]
+    owned = np.concatenate([p.gid[p.owned_local] for p in parts])
+    assert np.array_equal(np.sort(owned), np.arange(g.V))
+    for q in range(world):
+        pq = parts[q]
+        so = np.concatenate([[0], np.cumsum(pq.send_counts)])
+        for p in range(world):
+            pp = parts[p]
+            ro = np.concatenate([[0], np.cumsum(pp.recv_counts)])
+            sent = pq.gid[pq.send_local[so[p]:so[p + 1]]]
+            got = pp.gid[pp.recv_local[ro[q]:ro[q + 1]]]
+            assert np.array_equal(sent, got)
+        lg = pq.local_graph()
+        lg.rowptr.shape  # local rows: owned rows hold every global neighbour, ascending
+        for u in pq.owned_local[:20]:
+            nb_local = lg.colidx[lg.rowptr[u]:lg.rowptr[u + 1]]
+            assert np.array_equal(pq.gid[nb_local], g.neighbours(pq.gid[u]))
+
+
+def _rank_main(rank, world, port, kind, mode, M, thr, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (os.path.dirname(here), os.path.join(os.path.dirname(here), "python-p2p-network_amd"), here):
+        sys.path.insert(0, p)
+    import torch.distributed as dist
+    from p2pnetwork.gpu import PartitionedNetwork, TorchTransport, make_sources
+    from partition_mock import MockEngine
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = make_graph(kind)
+    src = make_sources(g.V, M, seed=11)
+    net = PartitionedNetwork(g, world, rank, TorchTransport(), mode=mode, fanout=3,
+                             gossip_seed=77, churn_threshold_value=thr, churn_seed=5,
+                             engine_factory=MockEngine)
+    net.broadcast(src)
+    rounds = net.run()
+    gids, seen = net.owned_planes()
+    _, hop, par = net.owned_hop_parent()
+    np.savez(os.path.join(out, f"rank{rank}.npz"), gids=gids, hop=hop, par=par,
+             relays=np.array([r.relays for r in rounds]), new=np.array([r.new_deliveries for r in rounds]),
+             words=np.array([r.active_words for r in rounds]), scatter=np.array([r.scatter_words for r in rounds]))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind,mode,M,thr,world", [
+    ("ws", "flood", 70, 0, 2),
+    ("ws", "flood", 64, 600_000_000, 3),
+    ("sparse", "flood", 40, 0, 2),
+    ("ba", "gossip", 64, 0, 2),
+    ("ws", "gossip", 30, 500_000_000, 3),
+])
+def test_partitioned_gloo_matches_oracle(kind, mode, M, thr, world):
+    import torch.multiprocessing as mp
+    from p2pnetwork.gpu import make_sources
+    g = make_graph(kind)
+    src = make_sources(g.V, M, seed=11)
+    with tempfile.TemporaryDirectory() as out:
+        mp.start_processes(_rank_main, args=(world, free_port(), kind, mode, M, thr, out), nprocs=world,
+                           start_method="spawn")
+        parts = [dict(np.load(os.path.join(out, f"rank{r}.npz"))) for r in range(world)]
+    hop = np.full((g.V, M), -1, np.int32)
+    par = np.full((g.V, M), -1, np.int32)
+    for p in parts:
+        hop[p["gids"]] = p["hop"]
+        par[p["gids"]] = p["par"]
+    if mode == "flood":
+        ora = relay_oracle.flood(g.rowptr, g.colidx, src, thr, 5)
+        np.testing.assert_array_equal(par, ora.parent)
+    else:
+        ora = relay_oracle.gossip(g.rowptr, g.colidx, src, 3, 77, 0, thr, 5)
+    np.testing.assert_array_equal(hop, ora.hop)
+    r0 = parts[0]
+    for p in parts[1:]:  # every rank reports the same global counters
+        for k in ("relays", "new", "words", "scatter"):
+            np.testing.assert_array_equal(p[k], r0[k])
+    np.testing.assert_array_equal(trim_zeros(r0["relays"]), trim_zeros([r["relays"] for r in ora.rounds]))
+    np.testing.assert_array_equal(trim_zeros(r0["new"]), trim_zeros([r["new_deliveries"] for r in ora.rounds]))
+    np.testing.assert_array_equal(trim_zeros(r0["words"]), trim_zeros([r["active_words"] for r in ora.rounds]))
+    np.testing.assert_array_equal(trim_zeros(r0["scatter"]), trim_zeros([r["scatter_words"] for r in ora.rounds]))
