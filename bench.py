@@ -36,7 +36,12 @@ WORKLOADS = {
                name="config3: 1M-peer Erdos-Renyi mean degree 16, 4096 flood broadcasts"),
     "c2": dict(graph="rrg", V=1000, a=8, M=64, mode="flood", fanout=3,
                name="config2: 1k-peer random 8-regular, 64 flood broadcasts"),
+    "c5": dict(graph="ws", V=100_000_000, a=8, beta=0.1, M=4096, mode="flood", fanout=3, churn=0.05,
+               partition=True,
+               name="config5: 100M-peer Watts-Strogatz k=8 beta=0.1, 4096 flood broadcasts, "
+                    "per-round edge-drop churn p=0.05, vertex-partitioned"),
 }
+GOSSIP_SEED, CHURN_SEED = 0x5EED, 0xC0FFEE
 
 KCLASS = ("seed", "flood_pull", "gossip_scatter_atomic", "record", "gossip_update", "gossip_pull",
           "gossip_scatter_store", "reserved")
@@ -100,10 +105,12 @@ def build_graph(w):
         return PeerGraph.gnp(w["V"], w["a"], seed=1)
     if w["graph"] == "rrg":
         return PeerGraph.random_regular(w["V"], int(w["a"]), seed=1)
+    if w["graph"] == "ws":
+        return PeerGraph.watts_strogatz(w["V"], int(w["a"]), w["beta"], seed=1)
     raise ValueError(w["graph"])
 
 
-def cpu_baseline(g, w, src, sample_msgs):
+def cpu_baseline(g, w, src, sample_msgs, thr):
     """The C oracle (oracle/relay_oracle.c, OpenMP) on a bounded sample of the same workload:
     the same graph with the first `sample_msgs` broadcasts.  Reported, not a target."""
     from oracle import coracle
@@ -111,7 +118,8 @@ def cpu_baseline(g, w, src, sample_msgs):
     os.environ["OMP_NUM_THREADS"] = str(threads)
     s = src[:sample_msgs]
     t0 = time.perf_counter()
-    res = coracle.run(g.rowptr, g.colidx, s, w["mode"], w["fanout"], 0x5EED, 0, 0, 0, record=False)
+    res = coracle.run(g.rowptr, g.colidx, s, w["mode"], w["fanout"], GOSSIP_SEED, 0, thr, CHURN_SEED,
+                      record=False)
     dt = time.perf_counter() - t0
     relays = sum(r["relays"] for r in res.rounds)
     return {"value": relays / dt / 1e9, "unit": "GTEPS", "cores": threads, "kind": "port",
@@ -138,6 +146,11 @@ def main():
     ap.add_argument("--workload", default="c4", choices=sorted(WORKLOADS))
     ap.add_argument("--cpu-sample-msgs", type=int, default=64)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--peers", type=int, default=0, help="override the workload's peer count "
+                    "(rehearsals only; the reported workload names the size actually run)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo stages the exchange through host memory (rehearsal with several "
+                         "ranks on one GPU); nccl = RCCL over xGMI")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -147,18 +160,36 @@ def main():
     if world > 1:
         import torch
         import torch.distributed as dist
+        local = local % max(torch.cuda.device_count(), 1)  # gloo rehearsal: ranks may share a GPU
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
 
     from p2pnetwork.gpu import GraphNetwork, make_sources
-    w = WORKLOADS[args.workload]
+    from p2pnetwork.gpu.network import churn_threshold
+    w = dict(WORKLOADS[args.workload])
+    if args.peers:
+        w["V"] = args.peers
+        w["name"] += f" [REDUCED: {args.peers} peers]"
+    thr = churn_threshold(w.get("churn", 0.0))
+    partitioned = bool(w.get("partition")) and world > 1
     t_gen = time.perf_counter()
     g = build_graph(w)
     t_gen = time.perf_counter() - t_gen
     M = w["M"]
-    src = make_sources(g.V, M, seed=1, msg_id_base=rank * M)
-    net = GraphNetwork(g, mode=w["mode"], fanout=w["fanout"], gossip_seed=0x5EED, timing=True,
-                       device=local, msg_id_base=rank * M)
+    common = dict(mode=w["mode"], fanout=w["fanout"], gossip_seed=GOSSIP_SEED, churn_threshold_value=thr,
+                  churn_seed=CHURN_SEED, timing=True, device=local)
+    if partitioned:
+        # one graph, vertex ranges per rank, boundary rows exchanged per round (RCCL all-to-all)
+        from p2pnetwork.gpu import PartitionedNetwork, TorchTransport
+        src = make_sources(g.V, M, seed=1)
+        net = PartitionedNetwork(g, world, rank, TorchTransport(device=torch.device("cuda", local)), **common)
+    else:
+        # message-axis replicas: rank r runs broadcasts r*M .. r*M+M-1 on its own graph copy
+        src = make_sources(g.V, M, seed=1, msg_id_base=rank * M)
+        net = GraphNetwork(g, msg_id_base=rank * M, **common)
     net.broadcast(src)
     for _ in range(args.warmup):
         net.reset()
@@ -185,16 +216,19 @@ def main():
     kt = net.kernel_times()  # reset() zeroes the timers: this is the LAST step's kernels
     if dist is not None:
         import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        red = f"cuda:{local}" if args.dist_backend == "nccl" else "cpu"
+        t = torch.tensor([elapsed], dtype=torch.float64, device=red)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        r = torch.tensor([relays], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(r, op=dist.ReduceOp.SUM)
-        relays = int(r.item())
+        if not partitioned:  # replicas: sum the ranks' relays (partitioned counters are global)
+            r = torch.tensor([relays], dtype=torch.float64, device=red)
+            dist.all_reduce(r, op=dist.ReduceOp.SUM)
+            relays = int(r.item())
     del kt0
 
     last = all_rounds[-1]
-    mb = model_bytes(last, w["mode"], (M + 63) // 64)
+    local_last = net.local_rounds if partitioned else last  # this rank's kernels' work
+    mb = model_bytes(local_last, w["mode"], (M + 63) // 64)
     dominant = max(KCLASS, key=lambda k: kt[k][0])
     dom_ms, dom_n = kt[dominant]
     achieved = mb[dominant] / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
@@ -209,13 +243,17 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if w.get("partition") else "weak",
         "vs_baseline": None,
         "dtype": "u64",
         "data": "synthetic (generated graph + Philox origins)",
-        "config": {"workload": w["name"], "peers": g.V, "edges": g.n_edges, "broadcasts_per_gpu": M,
-                   "mode": w["mode"], "fanout": w["fanout"], "rounds": len(last),
-                   "parallelism": f"message-axis replicas x{world}" if world > 1 else "single GPU"},
+        "config": {"workload": w["name"], "peers": g.V, "edges": g.n_edges,
+                   "broadcasts": M if w.get("partition") else M * world,
+                   "mode": w["mode"], "fanout": w["fanout"], "churn": w.get("churn", 0.0),
+                   "rounds": len(last),
+                   "parallelism": (f"vertex partition x{world} (RCCL all-to-all of boundary rows)"
+                                   if partitioned else
+                                   f"message-axis replicas x{world}" if world > 1 else "single GPU")},
         "roofline": {
             "bound": "hbm",
             "kernel": dominant,
@@ -234,10 +272,11 @@ def main():
         "survey_model_bytes_per_step": survey_bytes(last, w["mode"]),
         "kernel_time_frac_of_step": kernel_ms_total / (elapsed / args.steps * 1e3),
         "relays_per_step_per_gpu": relays / args.steps / world,
+        "exchange_ms_per_step": (net.exchange_s * 1e3) if partitioned else 0.0,
         "graph_gen_s": t_gen,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(g, w, src, args.cpu_sample_msgs)
+        out["cpu_baseline"] = cpu_baseline(g, w, src, args.cpu_sample_msgs, thr)
     net.close()
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -50,6 +50,10 @@ extern "C" {
 #define P2PG_FLAG_TIMING 2u /* per-kernel HIP-event timing (p2pg_kernel_times)              */
 #define P2PG_FLAG_NO_AUTOSTOP 4u /* partitioned runs: keep stepping after a locally quiet
                                     round (the caller decides global quiescence)          */
+#define P2PG_FLAG_LOCAL_GRAPH 8u /* rank-local graph of a vertex partition: ghost peers have
+                                    empty rows, so symmetry is checked between non-empty
+                                    rows only; gossip pushes use row atomics (no reverse
+                                    slots, no per-connection push plane)                   */
 
 typedef struct p2pg_engine p2pg_engine;
 typedef struct p2pg_graph p2pg_graph;

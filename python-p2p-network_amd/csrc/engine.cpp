@@ -292,7 +292,8 @@ int p2pg_load_csr(p2pg_engine* e, int64_t V, const int64_t* rowptr, const int32_
     }
   }
   // symmetry (every connection relays both ways, node.py:75-78) and reverse slots
-  std::vector<uint32_t> rev(e->cfg.mode == P2PG_MODE_GOSSIP && nnz < 0xFFFFFFFFll ? nnz : 0);
+  const bool local = (e->cfg.flags & P2PG_FLAG_LOCAL_GRAPH) != 0;
+  std::vector<uint32_t> rev(e->cfg.mode == P2PG_MODE_GOSSIP && !local && nnz < 0xFFFFFFFFll ? nnz : 0);
   int64_t asym = -1;
 #pragma omp parallel for schedule(dynamic, 4096)
   for (int64_t u = 0; u < V; ++u) {
@@ -300,6 +301,7 @@ int p2pg_load_csr(p2pg_engine* e, int64_t V, const int64_t* rowptr, const int32_
       const int64_t v = colidx[j];
       const int32_t* b = colidx + rowptr[v];
       const int32_t* en = colidx + rowptr[v + 1];
+      if (local && b == en) continue;  // ghost peer: its row lives on its owner rank
       const int32_t* it = std::lower_bound(b, en, (int32_t)u);
       if (it == en || *it != u) {
 #pragma omp critical

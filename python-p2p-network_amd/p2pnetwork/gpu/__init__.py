@@ -12,6 +12,9 @@ from ._lib import P2PGError, LIB_PATH
 from .graph import PeerGraph, make_sources
 from .network import GraphNetwork, RoundStats, Deliveries, churn_threshold
 from .partition import VertexPartition, PartitionedNetwork, TorchTransport
+from .compat import SimNode, SimConnection, CompatNetwork
+from . import wire
 
 __all__ = ["P2PGError", "LIB_PATH", "PeerGraph", "make_sources", "GraphNetwork", "RoundStats",
-           "Deliveries", "churn_threshold", "VertexPartition", "PartitionedNetwork", "TorchTransport"]
+           "Deliveries", "churn_threshold", "VertexPartition", "PartitionedNetwork", "TorchTransport",
+           "SimNode", "SimConnection", "CompatNetwork", "wire"]

@@ -17,6 +17,7 @@ MODE_GOSSIP = 1
 FLAG_RECORD = 1
 FLAG_TIMING = 2
 FLAG_NO_AUTOSTOP = 4
+FLAG_LOCAL_GRAPH = 8
 
 # graph kinds of p2pg_graph_generate
 GRAPH_RANDOM_REGULAR = 0

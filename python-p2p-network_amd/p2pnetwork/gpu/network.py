@@ -75,7 +75,7 @@ class GraphNetwork:
 
     def __init__(self, graph, mode="flood", fanout=3, gossip_seed=0x5EED, churn=0.0,
                  churn_threshold_value=None, churn_seed=0xC0FFEE, record=False, timing=False,
-                 device=0, msg_id_base=0, callback=None, autostop=True):
+                 device=0, msg_id_base=0, callback=None, autostop=True, local_graph=False):
         if not isinstance(graph, PeerGraph):
             raise TypeError("graph must be a PeerGraph")
         if mode not in ("flood", "gossip"):
@@ -94,7 +94,8 @@ class GraphNetwork:
                                   else churn_threshold(churn))
         cfg.msg_id_base = int(msg_id_base)
         cfg.flags = ((_lib.FLAG_RECORD if record else 0) | (_lib.FLAG_TIMING if timing else 0)
-                     | (0 if autostop else _lib.FLAG_NO_AUTOSTOP))
+                     | (0 if autostop else _lib.FLAG_NO_AUTOSTOP)
+                     | (_lib.FLAG_LOCAL_GRAPH if local_graph else 0))
         cfg.device = int(device)
         self.config = cfg
         L = _lib.lib()

@@ -17,6 +17,8 @@ Philox keys of gossip and churn use global ids: results are bit-identical to a s
 run.  A dummy, unconnected local peer (global id V) absorbs broadcasts whose origin is neither
 owned nor a ghost here.
 """
+import time
+
 import numpy as np
 
 from .graph import PeerGraph
@@ -139,10 +141,13 @@ class PartitionedNetwork:
         make = engine_factory or GraphNetwork
         self.net = make(self.part.local_graph(), mode=mode, fanout=fanout, gossip_seed=gossip_seed,
                         churn_threshold_value=churn_threshold_value, churn_seed=churn_seed,
-                        record=record, timing=timing, device=device, autostop=False)
+                        record=record, timing=timing, device=device, autostop=False,
+                        local_graph=True)
         self.net.set_global_ids(self.part.gid)
         self.net.set_exchange(self.part.send_local, self.part.recv_local)
-        self.rounds = []
+        self.rounds = []        # global counters (summed over ranks)
+        self.local_rounds = []  # this rank's engine counters (its owned peers' work)
+        self.exchange_s = 0.0   # host wall time spent in the row exchange since reset
         self.sources = None
 
     @property
@@ -152,11 +157,11 @@ class PartitionedNetwork:
     def broadcast(self, sources):
         self.sources = np.asarray(sources, dtype=np.int64)
         self.net.broadcast(self.part.local_sources(self.sources))
-        self.rounds = []
+        self.rounds, self.local_rounds, self.exchange_s = [], [], 0.0
 
     def reset(self):
         self.net.reset()
-        self.rounds = []
+        self.rounds, self.local_rounds, self.exchange_s = [], [], 0.0
 
     def _round0_stats(self):
         """Origination counted once, globally (every rank seeds origins it holds as ghosts)."""
@@ -189,7 +194,10 @@ class PartitionedNetwork:
 
     def step(self):
         st = self.net.step()
+        self.local_rounds.append(st)
+        t0 = time.perf_counter()
         self._exchange()
+        self.exchange_s += time.perf_counter() - t0
         if st.round == 0:
             g = self._round0_stats()
             # scatter words of round 0 are real local work (gossip): sum them
@@ -210,6 +218,13 @@ class PartitionedNetwork:
             if not st.new_deliveries:
                 break
         return out
+
+    @property
+    def message_count_send(self):
+        return sum(r.relays for r in self.rounds)
+
+    def kernel_times(self):
+        return self.net.kernel_times()
 
     def owned_planes(self):
         """(global ids, seen rows) of the peers this rank owns."""

@@ -1,5 +1,5 @@
 """Test-only NumPy stand-in for one rank's engine in a vertex-partitioned run (CPU tests of
-p2pnetwork.gpu.partition with the gloo backend).  It restates, on the rank-local graph with
+p2pnetwork.gpu.partition with the gloo backend, and of compat mode on one "rank").  It restates, on the rank-local graph with
 ghost rows, exactly the contract of the C-ABI's partition entry points (include/p2pgpu.h):
 frontier rows valid only with their A bit, ghost rows filled by unpack, pushes to ghosts moved
 by pack/unpack, Philox keys on global ids.  Uses the oracle's Philox (tests may)."""
@@ -27,7 +27,7 @@ def _bits(w, M):
 
 class MockEngine:
     def __init__(self, graph, mode="flood", fanout=3, gossip_seed=0, churn_threshold_value=0,
-                 churn_seed=0, record=False, timing=False, device=0, autostop=True):
+                 churn_seed=0, record=False, timing=False, device=0, autostop=True, local_graph=False):
         self.g, self.mode, self.k = graph, mode, fanout
         self.gseed, self.thr, self.cseed = gossip_seed, churn_threshold_value, churn_seed
         self.V = graph.V
@@ -150,6 +150,13 @@ class MockEngine:
             # a boundary peer appears once per neighbouring rank: OR, never overwrite
             # (the device unpack uses atomicOr); gossip parents are not checked when partitioned
             np.logical_or.at(self.next, self.send, b)
+
+    def deliveries(self, cap=None):
+        """this round's first receipts (unordered contract: callers sort)"""
+        from p2pnetwork.gpu.network import Deliveries
+        vs, ms = np.nonzero(self.F)
+        return Deliveries(vs.astype(np.int32), ms.astype(np.int32), self.hop[vs, ms].astype(np.int32),
+                          self.par[vs, ms].astype(np.int32))
 
     def seen_plane(self):
         return _words(self.seen)

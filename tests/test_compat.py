@@ -1,0 +1,107 @@
+"""Per-callback compat mode (p2pnetwork.gpu.compat): a Node-style dedup-relay app, written
+against the reference's hook surface, runs unchanged on CompatNetwork and reproduces the
+golden fixtures made with the reference's own Node objects (first-receipt round and sender per
+peer and message, total relays = sum of message_count_send).  CPU tests drive it with the
+test-only engine stand-in (tests/partition_mock.py); the gpu-marked ones with the HIP engine."""
+import numpy as np
+import pytest
+
+from conftest import golden_cases, load_golden
+from partition_mock import MockEngine
+
+
+def dedup_app():
+    from p2pnetwork.gpu.compat import SimNode
+
+    class DedupRelay(SimNode):  # the app of README.md:20 / examples, unchanged in shape
+        def __init__(self, host, port, id=None, callback=None, max_connections=0):
+            super().__init__(host, port, id, callback, max_connections)
+            self.seen = {}
+
+        def node_message(self, node, data):
+            mid = data["mid"]
+            if mid in self.seen:
+                return
+            self.seen[mid] = (self._net.current_round, int(node.id))
+            self.send_to_nodes(data, exclude=[node])
+
+    return DedupRelay
+
+
+def run_compat(z, factory=None):
+    from p2pnetwork.gpu import PeerGraph
+    from p2pnetwork.gpu.compat import CompatNetwork
+    g = PeerGraph(z["rowptr"], z["colidx"])
+    kw = dict(mode=str(z["mode"]), fanout=int(z["fanout"]), gossip_seed=int(z["gossip_seed"]),
+              churn_threshold_value=int(z["churn_threshold"]), churn_seed=int(z["churn_seed"]))
+    if factory is not None:
+        kw["engine_factory"] = factory
+    net = CompatNetwork(g, dedup_app(), **kw)
+    for m, s in enumerate(z["src"]):
+        net.nodes[int(s)].seen[m] = (0, -1)
+        net.nodes[int(s)].send_to_nodes({"mid": m})
+    net.run()
+    V, M = g.V, len(z["src"])
+    hop = np.full((V, M), -1, np.int32)
+    par = np.full((V, M), -1, np.int32)
+    for v, n in enumerate(net.nodes):
+        for m, (h, p) in n.seen.items():
+            hop[v, m], par[v, m] = h, p
+    sends = sum(n.message_count_send for n in net.nodes)
+    recv = sum(n.message_count_recv for n in net.nodes)
+    net.close()
+    return hop, par, sends, recv, net
+
+
+def check(z, hop, par, sends, recv):
+    np.testing.assert_array_equal(hop, z["hop"])
+    np.testing.assert_array_equal(par, z["parent"])
+    assert sends == int(z["round_relays"].sum())
+    assert recv == int((z["hop"] > 0).sum())  # first receipts (the origin gets no node_message)
+
+
+@pytest.mark.parametrize("name", golden_cases())
+def test_compat_mock_engine_matches_reference_golden(name):
+    z = load_golden(name)
+    hop, par, sends, recv, _ = run_compat(z, MockEngine)
+    check(z, hop, par, sends, recv)
+
+
+def test_compat_lifecycle_and_payload_codec():
+    from p2pnetwork.gpu import PeerGraph
+    from p2pnetwork.gpu.compat import CompatNetwork, SimNode
+    events = []
+
+    def cb(event, main_node, connected_node, data):
+        events.append((event, main_node.id, getattr(connected_node, "id", None), data))
+
+    g = PeerGraph.from_edges(4, [(0, 1), (1, 2), (2, 3)])
+    net = CompatNetwork(g, SimNode, node_kwargs={"callback": cb}, engine_factory=MockEngine)
+    assert [e[:3] for e in events] == [
+        ("outbound_node_connected", "0", "1"), ("inbound_node_connected", "1", "0"),
+        ("outbound_node_connected", "1", "2"), ("inbound_node_connected", "2", "1"),
+        ("outbound_node_connected", "2", "3"), ("inbound_node_connected", "3", "2")]
+    assert [c.id for c in net.nodes[1].all_nodes] == ["0", "2"]
+    events.clear()
+    net.nodes[0].send_to_nodes({"t": (1, 2)})   # tuple -> list through the JSON codec
+    net.nodes[3].send_to_nodes("42")             # a str holding JSON arrives parsed
+    net.nodes[3].send_to_nodes(12345)            # not sendable: counted, reaches nobody
+    net.run()
+    got = [(e[1], e[2], e[3]) for e in events if e[0] == "node_message"]
+    # round 1: peer 1 gets msg 0 from 0, peer 2 gets msg 1 from 3; round 2: 2<-1 (m0), 1<-2 (m1)
+    assert got == [("1", "0", {"t": [1, 2]}), ("2", "3", 42), ("1", "2", 42), ("2", "1", {"t": [1, 2]}),
+                   ("0", "1", 42), ("3", "2", {"t": [1, 2]})]
+    # flood relays: origin deg, others deg-1; the unsendable send counted 1 at peer 3
+    assert [n.message_count_send for n in net.nodes] == [1, 2, 2, 1 + 1]
+    assert [n.message_count_recv for n in net.nodes] == [1, 2, 2, 1]
+    net.nodes[2].stop()
+    assert events[-1][0] == "node_request_to_stop"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", golden_cases())
+def test_compat_gpu_engine_matches_reference_golden(name):
+    z = load_golden(name)
+    hop, par, sends, recv, net = run_compat(z)
+    check(z, hop, par, sends, recv)
+    assert net.absorbed_sends == recv if str(z["mode"]) == "flood" else True

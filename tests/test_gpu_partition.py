@@ -1,0 +1,143 @@
+"""GPU parity of the vertex-partitioned path: every rank is a real HIP engine (C-ABI
+partition entry points: global ids, exchange lists, pack/unpack kernels) on cuda:0, the ranks
+run as threads of one process and a thread transport stands in for the all-to-all.  The union
+of the owned results must equal the single-engine run and the oracle bit for bit."""
+import threading
+
+import numpy as np
+import pytest
+
+from conftest import trim_zeros
+from oracle import coracle, relay_oracle
+
+pytestmark = pytest.mark.gpu
+
+
+class ThreadTransport:
+    """all-to-all / sum-reduce among `world` threads of one process (device tensors)."""
+
+    def __init__(self, shared, rank):
+        self.s, self.rank = shared, rank
+
+    def _gather(self, item):
+        s = self.s
+        s["slots"][self.rank] = item
+        s["barrier"].wait()
+        items = list(s["slots"])
+        s["barrier"].wait()
+        return items
+
+    def alltoall_rows(self, send, send_counts, recv_counts, W):
+        import torch
+        torch.cuda.synchronize()
+        items = self._gather((send, np.asarray(send_counts)))
+        pieces = []
+        for buf, counts in items:
+            off = int(counts[:self.rank].sum()) * W
+            pieces.append(buf[off:off + int(counts[self.rank]) * W])
+        out = torch.cat(pieces) if pieces else send[:0]
+        assert out.numel() == int(np.sum(recv_counts)) * W
+        torch.cuda.synchronize()
+        return out
+
+    def allreduce_sum(self, values):
+        items = self._gather(np.asarray(values, dtype=np.int64))
+        return np.sum(items, axis=0)
+
+
+def run_partitioned(g, world, src, **kw):
+    from p2pnetwork.gpu import PartitionedNetwork
+    shared = {"slots": [None] * world, "barrier": threading.Barrier(world)}
+    results, errors = [None] * world, []
+
+    def rank_main(rank):
+        try:
+            net = PartitionedNetwork(g, world, rank, ThreadTransport(shared, rank), **kw)
+            with net.net:
+                net.broadcast(src)
+                rounds = net.run()
+                gids, seen = net.owned_planes()
+                hp = net.owned_hop_parent() if kw.get("record") else None
+            results[rank] = (rounds, gids, seen, hp)
+        except BaseException as exc:  # surface in the main thread; unblock the others
+            errors.append(exc)
+            shared["barrier"].abort()
+
+    th = [threading.Thread(target=rank_main, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=600)
+    if errors:
+        raise errors[0]
+    return results
+
+
+def assemble(results, V, W):
+    seen = np.zeros((V, W), dtype=np.uint64)
+    for _, gids, s, _ in results:
+        seen[gids] = s
+    return seen
+
+
+def graph(kind):
+    from p2pnetwork.gpu import PeerGraph
+    if kind == "ws":
+        return PeerGraph.watts_strogatz(20_000, 8, 0.1, seed=3)
+    if kind == "ba":
+        return PeerGraph.barabasi_albert(30_000, 4, seed=7)   # hubs at low ids -> hub kernels
+    return PeerGraph.gnp(5_000, 1.5, seed=2)                   # many small components
+
+
+@pytest.mark.parametrize("kind,mode,M,thr,world", [
+    ("ws", "flood", 64, 0, 2),
+    ("ws", "flood", 130, 400_000_000, 3),
+    ("ba", "flood", 200, 0, 4),
+    ("sparse", "flood", 65, 0, 3),
+    ("ws", "gossip", 64, 0, 2),
+    ("ba", "gossip", 96, 300_000_000, 3),
+    ("sparse", "gossip", 40, 0, 4),
+])
+def test_partitioned_engines_match_single_gpu(kind, mode, M, thr, world):
+    from p2pnetwork.gpu import GraphNetwork, make_sources
+    g = graph(kind)
+    src = make_sources(g.V, M, seed=21)
+    kw = dict(mode=mode, fanout=3, gossip_seed=99, churn_threshold_value=thr, churn_seed=17)
+    res = run_partitioned(g, world, src, record=(mode == "flood"), **kw)
+    with GraphNetwork(g, record=True, **kw) as one:
+        one.broadcast(src)
+        rounds1 = one.run()
+        seen1 = one.seen_plane()
+        hop1, par1 = one.hop_parent()
+    W = (M + 63) // 64
+    np.testing.assert_array_equal(assemble(res, g.V, W), seen1)
+    keys = ("new_deliveries", "relays", "active_vertices", "active_words", "wedges", "deg_active",
+            "scatter_words")
+    for rounds, *_ in res:  # every rank reports the global counters
+        for k in keys:
+            np.testing.assert_array_equal(trim_zeros([getattr(r, k) for r in rounds]),
+                                          trim_zeros([getattr(r, k) for r in rounds1]), err_msg=k)
+    if mode == "flood":
+        hop = np.full((g.V, M), -1, np.int32)
+        par = np.full((g.V, M), -1, np.int32)
+        for _, _, _, (gids, h, p) in res:
+            hop[gids], par[gids] = h, p
+        np.testing.assert_array_equal(hop, hop1)
+        np.testing.assert_array_equal(par, par1)
+    # and the single engine against the oracle (C restatement)
+    ora = coracle.run(g.rowptr, g.colidx, src, mode, 3, 99, 0, thr, 17, record=True)
+    np.testing.assert_array_equal(hop1, ora.hop)
+
+
+def test_partitioned_gossip_small_matches_numpy_oracle():
+    from p2pnetwork.gpu import PeerGraph, make_sources
+    g = PeerGraph.watts_strogatz(300, 6, 0.3, seed=1)
+    src = make_sources(g.V, 33, seed=2)
+    res = run_partitioned(g, 3, src, mode="gossip", fanout=2, gossip_seed=5,
+                          churn_threshold_value=900_000_000, churn_seed=8)
+    ora = relay_oracle.gossip(g.rowptr, g.colidx, src, 2, 5, 0, 900_000_000, 8)
+    seen = assemble(res, g.V, 1)
+    bits = np.unpackbits(seen.view(np.uint8), axis=1, bitorder="little")[:, :33].astype(bool)
+    np.testing.assert_array_equal(bits, ora.hop >= 0)
+    np.testing.assert_array_equal(trim_zeros([r.relays for r in res[0][0]]),
+                                  trim_zeros([r["relays"] for r in ora.rounds]))
