@@ -99,6 +99,28 @@ SIGNATURES = {
 _lib = None
 
 
+def _share_hip_runtime():
+    """Use PyTorch's HIP runtime when PyTorch is installed.
+
+    libp2pgpu.so links libamdhip64.so.7 from /opt/rocm; PyTorch ships its own build with the
+    same soname, and the first one loaded serves the whole process.  If ours came first,
+    PyTorch's later HIP initialisation fails ("No HIP GPUs are available"), so before loading
+    the engine the torch copy is preloaded (without importing torch).  Both the partitioned
+    path (RCCL via torch.distributed) and callers mixing torch tensors then share one runtime.
+    P2PG_HIP_RUNTIME=system keeps /opt/rocm's runtime (processes that never use torch)."""
+    if os.environ.get("P2PG_HIP_RUNTIME", "") == "system":
+        return
+    import importlib.util
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.submodule_search_locations:
+        return
+    for d in spec.submodule_search_locations:
+        p = os.path.join(d, "lib", "libamdhip64.so")
+        if os.path.exists(p):
+            ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL)
+            return
+
+
 def lib():
     """Load (once) and return the bound library; raises P2PGError if it is not built."""
     global _lib
@@ -107,6 +129,7 @@ def lib():
             raise P2PGError(
                 f"{LIB_PATH} is not built: run `make -C python-p2p-network_amd/csrc` "
                 "(or __graft_entry__.build()); there is no CPU fallback")
+        _share_hip_runtime()
         handle = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(handle, name)
