@@ -54,7 +54,6 @@ struct p2pg_engine {
   bool last_push_e = false;    // gossip: pushes of the previous round went to E (dense)
   double e_thresh = 0.1;       // store-mode when active words >= thresh * active rows * W
   int push_mode = 0;           // 0 auto, 1 always row atomics, 2 always edge stores
-  uint32_t ablate = 0;         // diagnostic kernel ablation (P2PG_ABLATE), wrong results
   int32_t* d_src = nullptr;
   DevState st{};
   size_t plane_bytes = 0, bm_bytes = 0;
@@ -142,7 +141,6 @@ RoundParams params(const p2pg_engine* e) {
   p.churn_thr = e->cfg.churn_threshold;
   p.cseed_lo = (uint32_t)e->cfg.churn_seed;
   p.cseed_hi = (uint32_t)(e->cfg.churn_seed >> 32);
-  p.ablate = e->ablate;
   return p;
 }
 
@@ -254,7 +252,6 @@ int p2pg_create(const p2pg_config* cfg, p2pg_engine** out) {
   p2pg_engine* e = new p2pg_engine;
   e->cfg = *cfg;
   if (const char* t = std::getenv("P2PG_E_THRESH")) e->e_thresh = std::atof(t);
-  if (const char* t = std::getenv("P2PG_ABLATE")) e->ablate = (uint32_t)std::atoi(t);
   if (const char* m = std::getenv("P2PG_GOSSIP_PUSH"))
     e->push_mode = !std::strcmp(m, "atomic") ? 1 : (!std::strcmp(m, "store") ? 2 : 0);
   HIPCHK(e, hipSetDevice(cfg->device));

@@ -70,6 +70,12 @@ __device__ __forceinline__ uint32_t gidx(const DevGraph& g, int64_t x) {
   return g.gid ? (uint32_t)g.gid[x] : (uint32_t)x;
 }
 
+// Same for a wave-uniform vertex: a scalar load (see ldc), no vmcnt wait.
+__device__ __forceinline__ uint32_t gidx_s(const DevGraph& g, int64_t x) {
+  const int64_t xu = __builtin_amdgcn_readfirstlane((int)x);
+  return g.gid ? (uint32_t)ldc(g.gid + xu) : (uint32_t)xu;
+}
+
 // wave index inside the block, forced into an SGPR so task indices stay scalar
 __device__ __forceinline__ int wave_in_block() {
   return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -573,18 +579,22 @@ __device__ __forceinline__ void wave_lds_sync() {
 // neighbours.  One wave per (source, GCHUNK-neighbour chunk):
 //   1. the row slice's active bits are compacted into an LDS list (prefix sum of popcounts),
 //      so the 64 lanes evaluate Philox + Floyd for equal shares of messages;
-//   2. picks landing in the chunk set bits of a GCHUNK x 64-word LDS mask table (LDS atomics);
+//   2. picks landing in the chunk set bits of a GCHUNK x 64-word LDS mask table (32-bit LDS
+//      atomics; table = [target][half][word], so the lanes of one batch -- distinct words,
+//      see the rank-major list -- hit distinct banks);
 //   3. flush, lane = word: every (target, word) mask leaves as part of one 512 B row access --
 //      STORE_E = false (sparse rounds): row atomicOr into the target's next row + T bit;
 //      STORE_E = true  (dense rounds):  plain store of the whole row (zeros included) into
 //      E[rev(slot)], the receiver's own slot of the connection, which the next round's
 //      k_pull1<GOSSIP> then streams contiguously per receiver.
+// Every per-source value (row offsets, global id, neighbour ids) is a scalar load or a lane
+// of a prefetched register: a vector load inside the loop would make the wave wait (vmcnt)
+// for its own in-flight row stores / atomics before every Philox batch.
 template <bool CHURN, int K, bool STORE_E>
 __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st, RoundParams p,
                                                         const int64_t* __restrict__ hub_items,
                                                         int64_t n_hub) {
-  // row stride 65 words: lanes ORing the same word into different targets hit different banks
-  __shared__ uint64_t tbl[WPB][GCHUNK][65];
+  __shared__ uint32_t tbl[WPB][GCHUNK][2][64];
   __shared__ uint16_t lst[WPB][GLIST];
   const int lane = threadIdx.x & 63;
   const int wib = wave_in_block();
@@ -600,10 +610,10 @@ __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st,
   const int k = K > 0 ? K : p.fanout;
   uint64_t c[STAT_N] = {0, 0, 0, 0, 0, 0, 0, 0};
 
-  // One (source v, neighbour chunk, row slice): f = this lane's frontier word, rv = lane j's
-  // receiver slot of connection nb + j (STORE_E only).
+  // One (source v, neighbour chunk, row slice): f = this lane's frontier word, nbr = lane j's
+  // neighbour nb + j -- its receiver slot (STORE_E) or its local id (row atomics).
   auto body = [&](int64_t v, int64_t rb, int64_t deg, int chunk, int sl, uint64_t f,
-                  uint32_t rv) {
+                  uint32_t nbr) {
     const int nb = chunk * GCHUNK;
     const int nn = (int)(deg - nb < GCHUNK ? deg - nb : GCHUNK);
     const bool all = deg <= k;
@@ -611,11 +621,15 @@ __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st,
     const bool valid = w < W;
     const bool anyf = __ballot(f != 0ull) != 0ull;
     if (!anyf && !STORE_E) return;
+    const uint32_t gv = gidx_s(g, v);
     if (anyf && !all) {
-      for (int j = 0; j < nn; ++j) tbl[wib][j][lane] = 0ull;
+      for (int j = 0; j < nn; ++j) {
+        tbl[wib][j][0][lane] = 0u;
+        tbl[wib][j][1][lane] = 0u;
+      }
       // rank-major compaction: list = every word's 1st set bit, then every word's 2nd set
-      // bit, ... so a 64-entry batch covers ~64 distinct words (distinct LDS table columns ->
-      // few bank conflicts), while every lane still gets equal Philox work
+      // bit, ... so a 64-entry batch covers ~64 distinct words (distinct LDS banks), while
+      // every lane still gets equal Philox work
       const uint32_t cnt = (uint32_t)__popcll(f);
       uint32_t maxc = cnt;
 #pragma unroll
@@ -648,28 +662,24 @@ __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st,
           const uint32_t e = lst[wib][i];
           const uint32_t wl = e >> 6, bit = e & 63u;
           const uint32_t mg = p.msg_base + (uint32_t)((sl * 64 + (int)wl) * 64) + bit;
+          uint32_t* const col = &tbl[wib][0][bit >> 5][wl];
+          const uint32_t mb = 1u << (bit & 31u);
           if constexpr (K > 0) {
             uint32_t pk[K];
-            if (p.ablate & 1u) {
-#pragma unroll
-              for (int q = 0; q < K; ++q) pk[q] = (mg * 7u + (uint32_t)q) % (uint32_t)deg;
-            } else {
-              gossip_picks_t<K>((uint32_t)p.round, gidx(g, v), mg, (uint32_t)deg, p.gseed_lo,
-                                p.gseed_hi, pk);
-            }
+            gossip_picks_t<K>((uint32_t)p.round, gv, mg, (uint32_t)deg, p.gseed_lo, p.gseed_hi,
+                              pk);
 #pragma unroll
             for (int q = 0; q < K; ++q) {
               const uint32_t jj = pk[q] - (uint32_t)nb;
-              if (jj < (uint32_t)nn && !(p.ablate & 4u))
-                atomicOr((unsigned long long*)&tbl[wib][jj][wl], 1ull << bit);
+              if (jj < (uint32_t)nn) atomicOr(col + jj * 128u, mb);
             }
           } else {
             uint32_t pk[16];
-            gossip_picks((uint32_t)p.round, gidx(g, v), mg, (uint32_t)deg, k, p.gseed_lo,
-                         p.gseed_hi, pk);
+            gossip_picks((uint32_t)p.round, gv, mg, (uint32_t)deg, k, p.gseed_lo, p.gseed_hi,
+                         pk);
             for (int q = 0; q < k; ++q) {
               const uint32_t jj = pk[q] - (uint32_t)nb;
-              if (jj < (uint32_t)nn) atomicOr((unsigned long long*)&tbl[wib][jj][wl], 1ull << bit);
+              if (jj < (uint32_t)nn) atomicOr(col + jj * 128u, mb);
             }
           }
         }
@@ -677,31 +687,39 @@ __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st,
       }
     }
     for (int j = 0; j < nn; ++j) {
-      const uint64_t x = all ? f : (anyf ? tbl[wib][j][lane] : 0ull);
+      const uint64_t x = all ? f
+                       : (anyf ? ((uint64_t)tbl[wib][j][1][lane] << 32) | tbl[wib][j][0][lane]
+                               : 0ull);
       const uint64_t bal = __ballot(x != 0ull);
+      const uint32_t nj = (uint32_t)__builtin_amdgcn_readlane((int)nbr, j);
       if (STORE_E) {
         bool dropped = false;
         if (CHURN && bal)
-          dropped = churn_dropped((uint32_t)p.round, gidx(g, v), gidx(g, g.colidx[rb + nb + j]),
+          dropped = churn_dropped((uint32_t)p.round, gv, gidx_s(g, ldc(g.colidx + rb + nb + j)),
                                   p.churn_thr, p.cseed_lo, p.cseed_hi);
         // receiver-major: the row lands in the RECEIVER's slot for this connection, so the
         // pull streams its own contiguous slot range
-        const uint32_t dslot = (uint32_t)__builtin_amdgcn_readlane((int)rv, j);
-        if (valid && !(p.ablate & 2u)) st.E[(int64_t)dslot * W + w] = dropped ? 0ull : x;
+        if (valid) st.E[(int64_t)nj * W + w] = dropped ? 0ull : x;
         if (!dropped && lane == 0) c[ST_SCATTER] += (uint64_t)__popcll(bal);
       } else {
         if (!bal) continue;
-        const int32_t u = g.colidx[rb + nb + j];
-        if (CHURN && churn_dropped((uint32_t)p.round, gidx(g, v), gidx(g, u), p.churn_thr,
+        const int64_t u = (int64_t)nj;
+        if (CHURN && churn_dropped((uint32_t)p.round, gv, gidx_s(g, u), p.churn_thr,
                                    p.cseed_lo, p.cseed_hi))
           continue;
-        if (x) atomicOr((unsigned long long*)&nx[(int64_t)u * W + w], (unsigned long long)x);
+        if (x) atomicOr((unsigned long long*)&nx[u * W + w], (unsigned long long)x);
         if (lane == 0) {
           atomicOr(&Tn[u >> 5], 1u << (u & 31));
           c[ST_SCATTER] += (uint64_t)__popcll(bal);
         }
       }
     }
+  };
+
+  // lane j's neighbour datum for the chunk starting at slot rb + nb
+  auto load_nbr = [&](int64_t rb, int nn) -> uint32_t {
+    if (lane >= nn) return 0u;
+    return STORE_E ? g.rev[rb + lane] : (uint32_t)g.colidx[rb + lane];
   };
 
   for (int64_t task = (int64_t)blockIdx.x * WPB + wib; task < ntasks;
@@ -731,7 +749,7 @@ __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st,
       uint32_t rv1 = 0;
       if (b1 >= 0) {
         if (lane < W) f1 = Fc[(base + b1) * W + lane];
-        if (STORE_E && lane < deg1) rv1 = g.rev[rb1 + lane];
+        rv1 = load_nbr(rb1, (int)deg1);
       }
       while (b1 >= 0) {
         const int b2 = pick_next(todo, rb2, deg2);
@@ -739,7 +757,7 @@ __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st,
         uint32_t rv2 = 0;
         if (b2 >= 0) {
           if (lane < W) f2 = Fc[(base + b2) * W + lane];
-          if (STORE_E && lane < deg2) rv2 = g.rev[rb2 + lane];
+          rv2 = load_nbr(rb2, (int)deg2);
         }
         body(base + b1, rb1, deg1, 0, 0, f1, rv1);
         b1 = b2;
@@ -772,8 +790,7 @@ __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st,
       if (task < nwords && deg > GCHUNK) continue;  // hub: handled by its chunk items
       const int nb = chunk * GCHUNK;
       const int nn = (int)(deg - nb < GCHUNK ? deg - nb : GCHUNK);
-      uint32_t rv = 0;
-      if (STORE_E && lane < nn) rv = g.rev[rb + nb + lane];
+      const uint32_t rv = load_nbr(rb + nb, nn);
       for (int sl = 0; sl < nslices; ++sl) {
         const int w = sl * 64 + lane;
         const uint64_t f = w < W ? Fc[v * W + w] : 0ull;
