@@ -106,6 +106,7 @@ void free_state(p2pg_engine* e) {
   dfree(s.hop);
   dfree(s.parent);
   dfree(s.E);
+  for (int i = 0; i < 2; ++i) dfree(s.AW[i]);
   dfree(s.stats);
   dfree(e->d_src);
   e->have_state = false;
@@ -218,8 +219,12 @@ int alloc_state(p2pg_engine* e) {
     // dense-round edge-mask buffer, only if it fits with headroom (else row atomics only)
     const size_t eb = (size_t)e->nnz * e->W * sizeof(uint64_t);
     size_t free_b = 0, total_b = 0;
-    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && eb + ((size_t)4 << 30) < free_b)
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && eb + ((size_t)4 << 30) < free_b) {
       if ((rc = A((void**)&s.E, eb ? eb : 8))) return rc;
+      if (e->W <= 64)  // packed E rows (see DevState::AW)
+        for (int i = 0; i < 2; ++i)
+          if ((rc = A((void**)&s.AW[i], sizeof(uint64_t) * (size_t)e->V))) return rc;
+    }
   }
   if (rec) {
     const size_t hb = (size_t)e->V * e->M * sizeof(int32_t);
@@ -432,6 +437,8 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
   uint64_t host_new = 0, host_relays = 0, host_av = 0, host_aw = 0, host_wedge = 0, host_degact = 0;
   if (e->round == 0) {
     if ((rc = timed(e, 0, [&] { return launch_zero_rows(s.F[0], e->W, e->d_src, e->M, e->stream); }))) return rc;
+    if (s.AW[0])
+      if ((rc = timed(e, 0, [&] { return launch_zero_rows(s.AW[0], 1, e->d_src, e->M, e->stream); }))) return rc;
     if ((rc = timed(e, 0, [&] { return launch_seed(s, e->d_src, e->M, e->stream); }))) return rc;
     // origination stats from the host copy of the sources
     std::vector<int64_t> vs(e->h_src.begin(), e->h_src.end());

@@ -22,6 +22,8 @@
 // so stats need few atomics.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "internal.h"
 #include "philox.h"
 
@@ -44,6 +46,21 @@ __device__ __forceinline__ uint64_t wave_sum(uint64_t x) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
   return x;
+}
+
+// Wave-wide 32-bit reductions through DPP row shifts and row broadcasts (gfx9 family):
+// four row_shr steps reduce each 16-lane row into its lane 15, row_bcast:15 / row_bcast:31
+// fold the rows into lane 63, which is then read as a scalar.
+template <bool MAX>
+__device__ __forceinline__ uint32_t wave_reduce_u32(uint32_t x) {
+  auto op = [](uint32_t a, uint32_t b) { return MAX ? (a > b ? a : b) : a + b; };
+  x = op(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false));
+  x = op(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false));
+  x = op(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false));
+  x = op(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false));
+  x = op(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false));
+  x = op(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false));
+  return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
 }
 
 __device__ __forceinline__ void flush_stats(unsigned long long* stats, const uint64_t* c,
@@ -100,6 +117,7 @@ __global__ void k_seed(DevState st, const int32_t* src, int32_t M) {
   atomicOr((unsigned long long*)&st.F[0][o], (unsigned long long)bit);
   atomicOr((unsigned long long*)&st.seen[o], (unsigned long long)bit);
   atomicOr(&st.A[0][v >> 5], 1u << (v & 31));
+  if (st.AW[0]) atomicOr((unsigned long long*)&st.AW[0][v], 1ull << (m >> 6));
 }
 
 // ---------------------------------------------------------------------------------------
@@ -235,7 +253,20 @@ struct PullStage {
   int32_t v;        // this lane's neighbour (first chunk)
   uint32_t r;       // its source row (flood: v, gossip: the slot itself)
   bool act;         // neighbour active (and its send not lost)
+  uint64_t am;      // packed E rows: the neighbour's active-word mask
 };
+
+// Word `lane` of a source row.  Packed E rows (gossip, st.AW) hold only the sender's active
+// words in order: word w sits at position popcount(am & ((1 << w) - 1)), absent if bit w of am
+// is clear (the sender had nothing in that word: the mask is zero).
+__device__ __forceinline__ uint64_t src_word(const uint64_t* __restrict__ Src, uint32_t row,
+                                             int W, int lane, bool packed, uint64_t am,
+                                             bool want) {
+  if (!packed) return want ? Src[(int64_t)row * W + lane] : 0ull;
+  const bool here = want && ((am >> lane) & 1ull);
+  const int pos = __popcll(am & ((1ull << lane) - 1ull));
+  return here ? Src[(int64_t)row * W + pos] : 0ull;
+}
 
 // Same computation as k_pull for W <= 64 (one row slice), software-pipelined two targets
 // deep so that a target costs ~one memory round trip instead of five: the task's 33 row
@@ -252,6 +283,8 @@ __global__ __launch_bounds__(256) void k_pull1(DevGraph g, DevState st, RoundPar
   const uint64_t* __restrict__ Src = GOSSIP ? st.E : st.F[prv];
   uint64_t* __restrict__ Fc = st.F[cur];
   const uint32_t* __restrict__ Ap = st.A[prv];
+  const uint64_t* __restrict__ AWp = GOSSIP ? st.AW[prv] : nullptr;
+  const bool packed = GOSSIP && AWp != nullptr;
   const int64_t ntasks = (V + 31) >> 5;
   const bool valid = lane < W;
   const uint64_t fm = valid ? full_mask(lane, W, st.M) : 0ull;
@@ -291,11 +324,13 @@ __global__ __launch_bounds__(256) void k_pull1(DevGraph g, DevState st, RoundPar
       if (q.b < 0) return;
       const int64_t j = q.beg + lane;
       bool a = false;
+      q.am = 0;
       if (j < q.end) {
         a = bit_test(Ap, q.v);
         if (CHURN && a)
           a = !churn_dropped((uint32_t)(p.round - 1), gidx(g, u0 + q.b), gidx(g, q.v),
                              p.churn_thr, p.cseed_lo, p.cseed_hi);
+        if (packed && a) q.am = AWp[q.v];
       }
       q.act = a;
     };
@@ -322,18 +357,22 @@ __global__ __launch_bounds__(256) void k_pull1(DevGraph g, DevState st, RoundPar
       if (__ballot(need != 0ull)) {
         uint64_t m = __ballot(s1.act);
         uint32_t srow = s1.r;
+        uint64_t sam = s1.am;
         int64_t cb = s1.beg;
         for (;;) {
           while (m) {
             uint32_t sv[8];
+            uint64_t am[8];
             bool ok[8];
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
               ok[k] = m != 0ull;
+              am[k] = 0ull;
               if (m) {
                 const int idx = __builtin_ctzll(m);
                 m &= m - 1ull;
                 sv[k] = (uint32_t)__builtin_amdgcn_readlane((int)srow, idx);
+                if (packed) am[k] = (uint64_t)readlane64((int64_t)sam, idx);
               } else {
                 sv[k] = 0u;
               }
@@ -341,7 +380,7 @@ __global__ __launch_bounds__(256) void k_pull1(DevGraph g, DevState st, RoundPar
             uint64_t x[8];
 #pragma unroll
             for (int k = 0; k < 8; ++k)
-              x[k] = (ok[k] && need) ? Src[(int64_t)sv[k] * W + lane] : 0ull;
+              x[k] = src_word(Src, sv[k], W, lane, packed, am[k], ok[k] && need);
 #pragma unroll
             for (int k = 0; k < 8; ++k) acc |= x[k];
           }
@@ -350,6 +389,7 @@ __global__ __launch_bounds__(256) void k_pull1(DevGraph g, DevState st, RoundPar
           const int64_t j = cb + lane;  // further chunks of a wide row: serial
           bool a = false;
           srow = 0;
+          sam = 0;
           if (j < s1.end) {
             const int32_t v = g.colidx[j];
             srow = GOSSIP ? (uint32_t)j : (uint32_t)v;
@@ -357,6 +397,7 @@ __global__ __launch_bounds__(256) void k_pull1(DevGraph g, DevState st, RoundPar
             if (CHURN && a)
               a = !churn_dropped((uint32_t)(p.round - 1), gidx(g, u), gidx(g, v), p.churn_thr,
                                  p.cseed_lo, p.cseed_hi);
+            if (packed && a) sam = AWp[v];
           }
           m = __ballot(a);
         }
@@ -376,7 +417,9 @@ __global__ __launch_bounds__(256) void k_pull1(DevGraph g, DevState st, RoundPar
       if (any) {
         if (valid) Fc[u * W + lane] = nw;
         aw |= 1u << s1.b;
+        const uint64_t wm = __ballot(nw != 0ull);
         if (lane == 0) {
+          if (GOSSIP && st.AW[cur]) st.AW[cur][u] = wm;
           c[ST_ACTIVE_V] += 1;
           c[ST_DEG_ACT] += deg;
         }
@@ -404,13 +447,15 @@ __global__ __launch_bounds__(256) void k_pull_hub_partial(DevGraph g, DevState s
   const int prv = (p.round & 1) ^ 1;
   const uint64_t* __restrict__ Src = GOSSIP ? st.E : st.F[prv];
   const uint32_t* __restrict__ Ap = st.A[prv];
+  const uint64_t* __restrict__ AWp = GOSSIP ? st.AW[prv] : nullptr;
+  const bool packed = GOSSIP && AWp != nullptr;
   const bool valid = lane < W;
   const uint64_t fm = valid ? full_mask(lane, W, st.M) : 0ull;
   for (int64_t it = (int64_t)blockIdx.x * WPB + wib; it < hp.n_items;
        it += (int64_t)gridDim.x * WPB) {
-    const int64_t packed = hp.items[it];
-    const int64_t u = packed >> 32;
-    const int64_t chunk = packed & 0xFFFFFFFFll;
+    const int64_t item = hp.items[it];
+    const int64_t u = item >> 32;
+    const int64_t chunk = item & 0xFFFFFFFFll;
     const int64_t rb = g.rowptr[u], re = g.rowptr[u + 1];
     const int64_t beg = rb + chunk * HUB_CHUNK;
     const int64_t end = beg + HUB_CHUNK < re ? beg + HUB_CHUNK : re;
@@ -420,6 +465,7 @@ __global__ __launch_bounds__(256) void k_pull_hub_partial(DevGraph g, DevState s
       for (int64_t cb = beg; cb < end; cb += 64) {
         const int64_t j = cb + lane;
         uint32_t srow = 0;
+        uint64_t sam = 0;
         bool a = false;
         if (j < end) {
           const int32_t v = g.colidx[j];
@@ -428,18 +474,22 @@ __global__ __launch_bounds__(256) void k_pull_hub_partial(DevGraph g, DevState s
           if (CHURN && a)
             a = !churn_dropped((uint32_t)(p.round - 1), gidx(g, u), gidx(g, v), p.churn_thr,
                                p.cseed_lo, p.cseed_hi);
+          if (packed && a) sam = AWp[v];
         }
         uint64_t m = __ballot(a);
         while (m) {
           uint32_t sv[8];
+          uint64_t am[8];
           bool ok[8];
 #pragma unroll
           for (int k = 0; k < 8; ++k) {
             ok[k] = m != 0ull;
+            am[k] = 0ull;
             if (m) {
               const int idx = __builtin_ctzll(m);
               m &= m - 1ull;
               sv[k] = (uint32_t)__builtin_amdgcn_readlane((int)srow, idx);
+              if (packed) am[k] = (uint64_t)readlane64((int64_t)sam, idx);
             } else {
               sv[k] = 0u;
             }
@@ -447,7 +497,7 @@ __global__ __launch_bounds__(256) void k_pull_hub_partial(DevGraph g, DevState s
           uint64_t x[8];
 #pragma unroll
           for (int k = 0; k < 8; ++k)
-            x[k] = (ok[k] && need) ? Src[(int64_t)sv[k] * W + lane] : 0ull;
+            x[k] = src_word(Src, sv[k], W, lane, packed, am[k], ok[k] && need);
 #pragma unroll
           for (int k = 0; k < 8; ++k) acc |= x[k];
         }
@@ -491,7 +541,9 @@ __global__ __launch_bounds__(256) void k_pull_hub_finalize(DevGraph g, DevState 
     }
     if (__ballot(nw != 0ull)) {
       if (valid) st.F[cur][u * W + lane] = nw;
+      const uint64_t wm = __ballot(nw != 0ull);
       if (lane == 0) {
+        if (GOSSIP && st.AW[cur]) st.AW[cur][u] = wm;
         atomicOr(&st.A[cur][u >> 5], 1u << (u & 31));
         c[ST_ACTIVE_V] += 1;
         c[ST_DEG_ACT] += deg;
@@ -544,8 +596,10 @@ __global__ __launch_bounds__(256) void k_gossip_update(DevGraph g, DevState st,
           }
         }
         const uint64_t nw = x & ~s;
-        const bool any = __ballot(nw != 0ull) != 0ull;
+        const uint64_t wm = __ballot(nw != 0ull);
+        const bool any = wm != 0ull;
         row_new |= any;
+        if (any && nslices == 1 && st.AW[cur] && lane == 0) st.AW[cur][u] = wm;
         if (nw) st.seen[u * W + w] = s | nw;
         if (valid && (any || nslices > 1)) Fc[u * W + w] = nw;
         if (nw) {
@@ -610,6 +664,33 @@ __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st,
   const int k = K > 0 ? K : p.fanout;
   uint64_t c[STAT_N] = {0, 0, 0, 0, 0, 0, 0, 0};
 
+  // Philox + Floyd for list entries [0, n) of this wave, picks ORed into the LDS table.
+  auto pick_batch = [&](auto check_v, uint32_t n, int sl, uint32_t gv, int64_t deg, int nb,
+                        int nn) {
+    constexpr bool CHECK = decltype(check_v)::value;
+    auto one = [&](uint32_t e, bool ok) {
+      const uint32_t wl = e >> 6, bit = e & 63u;
+      const uint32_t mg = p.msg_base + (uint32_t)((sl * 64 + (int)wl) * 64) + bit;
+      uint32_t* const col = &tbl[wib][0][bit >> 5][wl];
+      const uint32_t mb = 1u << (bit & 31u);
+      uint32_t pk[K > 0 ? K : 1];
+      gossip_picks_t<(K > 0 ? K : 1)>((uint32_t)p.round, gv, mg, (uint32_t)deg, p.gseed_lo,
+                                      p.gseed_hi, pk);
+#pragma unroll
+      for (int q = 0; q < (K > 0 ? K : 1); ++q) {
+        const uint32_t jj = pk[q] - (uint32_t)nb;
+        if (ok && (!CHECK || jj < (uint32_t)nn)) atomicOr(col + jj * 128u, mb);
+      }
+    };
+    // the next batch's list entry is read before this batch's Philox (hides the LDS trip)
+    uint32_t en = (uint32_t)lane < n ? lst[wib][lane] : 0u;
+    for (uint32_t i = lane; i < n; i += 64) {
+      const uint32_t e = en;
+      en = i + 64 < n ? lst[wib][i + 64] : 0u;
+      one(e, true);
+    }
+  };
+
   // One (source v, neighbour chunk, row slice): f = this lane's frontier word, nbr = lane j's
   // neighbour nb + j -- its receiver slot (STORE_E) or its local id (row atomics).
   auto body = [&](int64_t v, int64_t rb, int64_t deg, int chunk, int sl, uint64_t f,
@@ -619,7 +700,8 @@ __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st,
     const bool all = deg <= k;
     const int w = sl * 64 + lane;
     const bool valid = w < W;
-    const bool anyf = __ballot(f != 0ull) != 0ull;
+    const uint64_t fam = __ballot(f != 0ull);  // active words of this slice
+    const bool anyf = fam != 0ull;
     if (!anyf && !STORE_E) return;
     const uint32_t gv = gidx_s(g, v);
     if (anyf && !all) {
@@ -631,15 +713,8 @@ __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st,
       // bit, ... so a 64-entry batch covers ~64 distinct words (distinct LDS banks), while
       // every lane still gets equal Philox work
       const uint32_t cnt = (uint32_t)__popcll(f);
-      uint32_t maxc = cnt;
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        const uint32_t t = __shfl_xor(maxc, o);
-        maxc = t > maxc ? t : maxc;
-      }
-      maxc = __builtin_amdgcn_readfirstlane(maxc);
-      const uint32_t total =
-          __builtin_amdgcn_readfirstlane((uint32_t)wave_sum((uint64_t)cnt));
+      const uint32_t maxc = wave_reduce_u32<true>(cnt);
+      const uint32_t total = wave_reduce_u32<false>(cnt);
       for (uint32_t lb = 0; lb < total; lb += GLIST) {
         uint64_t ff = f;
         uint32_t base = 0;
@@ -658,22 +733,19 @@ __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st,
         }
         wave_lds_sync();
         const uint32_t n = total - lb < (uint32_t)GLIST ? total - lb : (uint32_t)GLIST;
-        for (uint32_t i = lane; i < n; i += 64) {
-          const uint32_t e = lst[wib][i];
-          const uint32_t wl = e >> 6, bit = e & 63u;
-          const uint32_t mg = p.msg_base + (uint32_t)((sl * 64 + (int)wl) * 64) + bit;
-          uint32_t* const col = &tbl[wib][0][bit >> 5][wl];
-          const uint32_t mb = 1u << (bit & 31u);
-          if constexpr (K > 0) {
-            uint32_t pk[K];
-            gossip_picks_t<K>((uint32_t)p.round, gv, mg, (uint32_t)deg, p.gseed_lo, p.gseed_hi,
-                              pk);
-#pragma unroll
-            for (int q = 0; q < K; ++q) {
-              const uint32_t jj = pk[q] - (uint32_t)nb;
-              if (jj < (uint32_t)nn) atomicOr(col + jj * 128u, mb);
-            }
-          } else {
+        if constexpr (K > 0) {
+          // a source whose whole adjacency is this chunk needs no range check on its picks
+          if (nb == 0 && nn == (int)deg)
+            pick_batch(std::false_type{}, n, sl, gv, deg, nb, nn);
+          else
+            pick_batch(std::true_type{}, n, sl, gv, deg, nb, nn);
+        } else {
+          for (uint32_t i = lane; i < n; i += 64) {
+            const uint32_t e = lst[wib][i];
+            const uint32_t wl = e >> 6, bit = e & 63u;
+            const uint32_t mg = p.msg_base + (uint32_t)((sl * 64 + (int)wl) * 64) + bit;
+            uint32_t* const col = &tbl[wib][0][bit >> 5][wl];
+            const uint32_t mb = 1u << (bit & 31u);
             uint32_t pk[16];
             gossip_picks((uint32_t)p.round, gv, mg, (uint32_t)deg, k, p.gseed_lo, p.gseed_hi,
                          pk);
@@ -686,10 +758,14 @@ __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st,
         wave_lds_sync();
       }
     }
+    const bool use_tbl = anyf && !all;
+    auto tbl_row = [&](int j) -> uint64_t {
+      return ((uint64_t)tbl[wib][j][1][lane] << 32) | tbl[wib][j][0][lane];
+    };
+    uint64_t xn = use_tbl && nn > 0 ? tbl_row(0) : 0ull;
     for (int j = 0; j < nn; ++j) {
-      const uint64_t x = all ? f
-                       : (anyf ? ((uint64_t)tbl[wib][j][1][lane] << 32) | tbl[wib][j][0][lane]
-                               : 0ull);
+      const uint64_t x = all ? f : xn;  // row j; row j + 1 is read before row j is stored
+      if (use_tbl && j + 1 < nn) xn = tbl_row(j + 1);
       const uint64_t bal = __ballot(x != 0ull);
       const uint32_t nj = (uint32_t)__builtin_amdgcn_readlane((int)nbr, j);
       if (STORE_E) {
@@ -698,8 +774,15 @@ __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st,
           dropped = churn_dropped((uint32_t)p.round, gv, gidx_s(g, ldc(g.colidx + rb + nb + j)),
                                   p.churn_thr, p.cseed_lo, p.cseed_hi);
         // receiver-major: the row lands in the RECEIVER's slot for this connection, so the
-        // pull streams its own contiguous slot range
-        if (valid) st.E[(int64_t)nj * W + w] = dropped ? 0ull : x;
+        // pull streams its own contiguous slot range; packed: only the active words, in order
+#ifdef P2PG_DIAG_NO_ESTORE  // diagnostic build only (wrong results): the stores' cost
+        if (p.round < 0)
+#endif
+        if (st.AW[cur]) {
+          if (f) st.E[(int64_t)nj * W + __popcll(fam & ((1ull << lane) - 1ull))] = dropped ? 0ull : x;
+        } else if (valid) {
+          st.E[(int64_t)nj * W + w] = dropped ? 0ull : x;
+        }
         if (!dropped && lane == 0) c[ST_SCATTER] += (uint64_t)__popcll(bal);
       } else {
         if (!bal) continue;

@@ -10,7 +10,8 @@ import os
 import numpy as np
 
 LIB_NAME = "libp2pgpu.so"
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+# P2PG_LIB: load another build of the library (A/B comparisons of kernel variants)
+LIB_PATH = os.environ.get("P2PG_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 
 MODE_FLOOD = 0
 MODE_GOSSIP = 1
