@@ -274,7 +274,11 @@ __device__ __forceinline__ uint64_t src_word(const uint64_t* __restrict__ Src, u
 // target t+1's activity gather (A bits of its neighbours) is issued, before target t's rows
 // are loaded, and all three wait together.  Hub targets (g.H) are left to k_pull_hub_*.
 template <bool CHURN, bool GOSSIP>
-__global__ __launch_bounds__(256) void k_pull1(DevGraph g, DevState st, RoundParams p) {
+#ifndef P2PG_PULL_WAVES
+#define P2PG_PULL_WAVES 1
+#endif
+__global__ __launch_bounds__(256, P2PG_PULL_WAVES) void k_pull1(DevGraph g, DevState st,
+                                                                RoundParams p) {
   const int lane = threadIdx.x & 63;
   const int wib = wave_in_block();
   const int64_t V = g.V;
@@ -326,11 +330,12 @@ __global__ __launch_bounds__(256) void k_pull1(DevGraph g, DevState st, RoundPar
       bool a = false;
       q.am = 0;
       if (j < q.end) {
+        // issued with (not after) the activity bit: both depend only on the neighbour id
+        if (packed) q.am = AWp[q.v];
         a = bit_test(Ap, q.v);
         if (CHURN && a)
           a = !churn_dropped((uint32_t)(p.round - 1), gidx(g, u0 + q.b), gidx(g, q.v),
                              p.churn_thr, p.cseed_lo, p.cseed_hi);
-        if (packed && a) q.am = AWp[q.v];
       }
       q.act = a;
     };
