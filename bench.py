@@ -44,27 +44,52 @@ WORKLOADS = {
 GOSSIP_SEED, CHURN_SEED = 0x5EED, 0xC0FFEE
 
 KCLASS = ("seed", "flood_pull", "gossip_scatter_atomic", "record", "gossip_update", "gossip_pull",
-          "gossip_scatter_store", "reserved")
+          "gossip_scatter_store", "gossip_fused")
+ATOMIC, EDGE, FUSED = 1, 2, 3  # p2pg_round_stats.push_form (include/p2pgpu.h P2PG_PUSH_*)
 
 
-def model_bytes(rounds, mode, W):
+def push_forms(rounds):
+    """Each gossip round's push form; from the engine (push_form) when it reports one, else
+    read off the next round (touched_words > 0 <=> the pushes went by row atomics)."""
+    n = len(rounds)
+    out = []
+    for i, r in enumerate(rounds):
+        f = getattr(r, "push_form", 0)
+        if not f:
+            f = EDGE if (i + 1 < n and rounds[i + 1].touched_words == 0 and r.active_vertices > 0) \
+                else ATOMIC
+        out.append(f)
+    return out
+
+
+def model_bytes(rounds, mode, W, packed=None):
     """Algorithmic HBM bytes per kernel class for one run.
 
     flood pull, round r:  8*wedges[r-1] + 8*words[r-1] + 4*degact[r-1]
                                         + 8*peers[r-1] + 24*words[r]
-    gossip scatter, round r:            8*words[r] + 8*peers[r] + 4*degact[r]
-                                        + sparse form: 16*scatter[r] (read-modify-write of
-                                          each pushed word by a row atomicOr)
-                                        + dense form:  8*W*degact[r] (every connection row of
-                                          an active sender is stored whole)
-    gossip consume, round r >= 1:       after a sparse round: 24*touched[r] + 16*words[r]
-                                        after a dense round:  8*W*degact[r-1] + 24*words[r]
-    A round's push form is read off the next round: touched_words > 0 <=> row atomics.
+    gossip, pushes of round r:          atomic: 8*words[r] + 8*peers[r] + 4*degact[r]
+                                                + 16*scatter[r] (read-modify-write of each
+                                                pushed word by a row atomicOr)
+                                        edge:   8*words[r] + 8*peers[r] + 4*degact[r]
+                                                + 8*wedges[r] (packed E rows, W <= 64: each
+                                                connection of an active sender gets the
+                                                sender's active words only; 8*W*degact[r]
+                                                unpacked)
+    gossip, arrivals of round r >= 1:   after atomic pushes (update): 24*touched[r] + 16*words[r]
+                                        after edge pushes (pull):     8*wedges[r-1] (packed;
+                                                unpacked 8*W*degact[r-1]) + 24*words[r]
+    fused round r (pull + pushes in one pass, gossip_fused):
+                                        8*wedges[r-1] + 24*words[r] + 4*degact[r] + 8*wedges[r]
+                                        (the frontier row is not re-read: no 8*words[r])
     """
     b = {k: 0 for k in KCLASS}
-    n = len(rounds)
-    dense = [i + 1 < n and rounds[i + 1].touched_words == 0 and rounds[i].active_vertices > 0
-             for i in range(n)]
+    if packed is None:
+        packed = W <= 64
+    forms = push_forms(rounds) if mode == "gossip" else []
+
+    def e_bytes(r):
+        return 8 * (r.wedges if packed else W * r.deg_active)
+
     for i, r in enumerate(rounds):
         if mode == "flood":
             if i >= 1:
@@ -72,14 +97,18 @@ def model_bytes(rounds, mode, W):
                 b["flood_pull"] += (8 * p.wedges + 8 * p.active_words + 4 * p.deg_active
                                     + 8 * p.active_vertices + 24 * r.active_words)
             continue
+        if forms[i] == FUSED:
+            b["gossip_fused"] += (e_bytes(rounds[i - 1]) + 24 * r.active_words + 4 * r.deg_active
+                                  + e_bytes(r))
+            continue
         if i >= 1:
-            if dense[i - 1]:
-                b["gossip_pull"] += 8 * W * rounds[i - 1].deg_active + 24 * r.active_words
+            if forms[i - 1] in (EDGE, FUSED):
+                b["gossip_pull"] += e_bytes(rounds[i - 1]) + 24 * r.active_words
             else:
                 b["gossip_update"] += 24 * r.touched_words + 16 * r.active_words
         common = 8 * r.active_words + 8 * r.active_vertices + 4 * r.deg_active
-        if dense[i]:
-            b["gossip_scatter_store"] += common + 8 * W * r.deg_active
+        if forms[i] == EDGE:
+            b["gossip_scatter_store"] += common + e_bytes(r)
         else:
             b["gossip_scatter_atomic"] += common + 16 * r.scatter_words
     return b

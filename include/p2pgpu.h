@@ -46,6 +46,11 @@ extern "C" {
 #define P2PG_MODE_FLOOD 0  /* forward to all connections except the sender (node.py:106-112) */
 #define P2PG_MODE_GOSSIP 1 /* push-gossip: k Philox-chosen connections      */
 
+#define P2PG_PUSH_NONE 0   /* flood, or nothing pushed                                   */
+#define P2PG_PUSH_ATOMIC 1 /* gossip sparse round: row atomicOr into the targets' rows    */
+#define P2PG_PUSH_EDGE 2   /* gossip dense round: per-connection mask stores (E plane)    */
+#define P2PG_PUSH_FUSED 3  /* as EDGE, in one pass with this round's pull of E            */
+
 #define P2PG_FLAG_RECORD 1u /* keep hop/parent planes [V][M] (validation scale)            */
 #define P2PG_FLAG_TIMING 2u /* per-kernel HIP-event timing (p2pg_kernel_times)              */
 #define P2PG_FLAG_NO_AUTOSTOP 4u /* partitioned runs: keep stepping after a locally quiet
@@ -81,6 +86,8 @@ typedef struct p2pg_round_stats {
   uint64_t deg_active;       /* sum over A_r of deg(peer)                                 */
   uint64_t scatter_words;    /* gossip: nonzero (sender, target, word) masks pushed       */
   uint64_t touched_words;    /* gossip: nonzero pushed-to words consumed in round r       */
+  int32_t push_form;         /* gossip: how round r's pushes left (P2PG_PUSH_*); flood 0    */
+  int32_t reserved_;
 } p2pg_round_stats;
 
 /* ---- graphs (host side; no GPU needed) ---------------------------------------------- */
@@ -122,7 +129,8 @@ int p2pg_read_planes(p2pg_engine* e, uint64_t* seen, int32_t* hop, int32_t* pare
 /* Summed device time per kernel class since the last reset (needs P2PG_FLAG_TIMING):
  * 0 seed (origination), 1 flood pull, 2 gossip scatter by row atomics (sparse rounds),
  * 3 record (validation), 4 gossip update (consume row atomics), 5 gossip pull (consume edge
- * stores), 6 gossip scatter by edge stores (dense rounds), 7 reserved.                   */
+ * stores), 6 gossip scatter by edge stores (dense rounds), 7 gossip fused pull + scatter
+ * (a dense round after a dense round).                                                  */
 #define P2PG_KCLASS_N 8
 int p2pg_kernel_times(p2pg_engine* e, double ms[P2PG_KCLASS_N], int64_t launches[P2PG_KCLASS_N]);
 /* ---- vertex-partitioned runs (one engine per GPU) ---------------------

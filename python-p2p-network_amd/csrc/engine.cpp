@@ -10,6 +10,9 @@
 //   flood  r >= 1  pull:   F[r&1], A[r&1], seen <- OR of active neighbours' F[(r-1)&1]
 //   gossip r >= 1  update: F[r&1], A[r&1], seen <- next[r&1] & ~seen  (T[r&1] = touched rows)
 //   gossip r >= 0  scatter: next[(r+1)&1], T[(r+1)&1] |= k Philox picks of every F[r&1] bit
+//                  (sparse rounds), or E[r&1] per-connection masks (dense rounds; the next
+//                  round pulls them; a dense round after a dense round runs pull + scatter
+//                  as one fused pass, k_gossip_fused)
 //   record         hop/parent planes for the bits of F[r&1]   (P2PG_FLAG_RECORD only)
 #include <hip/hip_runtime.h>
 
@@ -37,6 +40,8 @@ struct p2pg_engine {
   int32_t* d_colidx = nullptr;
   int64_t* d_hub = nullptr;
   int64_t n_hub = 0;
+  int64_t* d_hub_big = nullptr;  // the chunk items of sources with deg > HUB_T (fused rounds)
+  int64_t n_hub_big = 0;
   uint32_t* d_rev = nullptr;   // gossip: reverse edge slots
   // pull hub split (deg > HUB_T)
   uint32_t* d_H = nullptr;
@@ -54,6 +59,8 @@ struct p2pg_engine {
   bool last_push_e = false;    // gossip: pushes of the previous round went to E (dense)
   double e_thresh = 0.1;       // store-mode when active words >= thresh * active rows * W
   int push_mode = 0;           // 0 auto, 1 always row atomics, 2 always edge stores
+  bool fused = true;           // dense rounds after dense rounds: one pull+scatter pass
+  uint64_t prev_aw = 0, prev_av = 0;  // active words / rows of the previous round
   int32_t* d_src = nullptr;
   DevState st{};
   size_t plane_bytes = 0, bm_bytes = 0;
@@ -105,7 +112,8 @@ void free_state(p2pg_engine* e) {
   dfree(s.S);
   dfree(s.hop);
   dfree(s.parent);
-  dfree(s.E);
+  if (s.E[1] == s.E[0]) s.E[1] = nullptr;
+  for (int i = 0; i < 2; ++i) dfree(s.E[i]);
   for (int i = 0; i < 2; ++i) dfree(s.AW[i]);
   dfree(s.stats);
   dfree(e->d_src);
@@ -116,6 +124,7 @@ void free_graph(p2pg_engine* e) {
   dfree(e->d_rowptr);
   dfree(e->d_colidx);
   dfree(e->d_hub);
+  dfree(e->d_hub_big);
   dfree(e->d_rev);
   dfree(e->d_H);
   dfree(e->d_hub_items);
@@ -129,6 +138,7 @@ void free_graph(p2pg_engine* e) {
   e->n_send = e->n_recv = 0;
   e->hp = HubPlan{};
   e->n_hub = 0;
+  e->n_hub_big = 0;
 }
 
 RoundParams params(const p2pg_engine* e) {
@@ -220,10 +230,16 @@ int alloc_state(p2pg_engine* e) {
     const size_t eb = (size_t)e->nnz * e->W * sizeof(uint64_t);
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && eb + ((size_t)4 << 30) < free_b) {
-      if ((rc = A((void**)&s.E, eb ? eb : 8))) return rc;
-      if (e->W <= 64)  // packed E rows (see DevState::AW)
+      if ((rc = A((void**)&s.E[0], eb ? eb : 8))) return rc;
+      s.E[1] = s.E[0];
+      if (e->W <= 64) {  // packed E rows (see DevState::AW)
         for (int i = 0; i < 2; ++i)
           if ((rc = A((void**)&s.AW[i], sizeof(uint64_t) * (size_t)e->V))) return rc;
+        // second E plane for fused dense rounds (round r pulls E[(r-1)&1], pushes E[r&1])
+        if (e->fused && hipMemGetInfo(&free_b, &total_b) == hipSuccess &&
+            eb + ((size_t)4 << 30) < free_b)
+          if ((rc = A((void**)&s.E[1], eb ? eb : 8))) return rc;
+      }
     }
   }
   if (rec) {
@@ -257,6 +273,7 @@ int p2pg_create(const p2pg_config* cfg, p2pg_engine** out) {
   p2pg_engine* e = new p2pg_engine;
   e->cfg = *cfg;
   if (const char* t = std::getenv("P2PG_E_THRESH")) e->e_thresh = std::atof(t);
+  if (const char* f = std::getenv("P2PG_FUSED")) e->fused = std::strcmp(f, "0") != 0;
   if (const char* m = std::getenv("P2PG_GOSSIP_PUSH"))
     e->push_mode = !std::strcmp(m, "atomic") ? 1 : (!std::strcmp(m, "store") ? 2 : 0);
   HIPCHK(e, hipSetDevice(cfg->device));
@@ -329,13 +346,17 @@ int p2pg_load_csr(p2pg_engine* e, int64_t V, const int64_t* rowptr, const int32_
   HIPCHK(e, hipMemcpy(e->d_rowptr, rowptr, sizeof(int64_t) * (V + 1), hipMemcpyHostToDevice));
   if (nnz) HIPCHK(e, hipMemcpy(e->d_colidx, colidx, sizeof(int32_t) * nnz, hipMemcpyHostToDevice));
   // gossip: (source, neighbour-chunk) items for sources wider than one chunk
-  std::vector<int64_t> hub;
+  std::vector<int64_t> hub, hub_big;
   for (int64_t v = 0; v < V; ++v) {
     const int64_t d = rowptr[v + 1] - rowptr[v];
     if (d > GCHUNK)
-      for (int64_t c = 0; c * GCHUNK < d; ++c) hub.push_back((v << 32) | c);
+      for (int64_t c = 0; c * GCHUNK < d; ++c) {
+        hub.push_back((v << 32) | c);
+        if (d > HUB_T) hub_big.push_back((v << 32) | c);
+      }
   }
   e->n_hub = (int64_t)hub.size();
+  e->n_hub_big = (int64_t)hub_big.size();
   {  // pull-side hub plan
     std::vector<int32_t> hubs;
     std::vector<int64_t> items, begin{0};
@@ -365,6 +386,9 @@ int p2pg_load_csr(p2pg_engine* e, int64_t V, const int64_t* rowptr, const int32_
   HIPCHK(e, hipMalloc((void**)&e->d_hub, sizeof(int64_t) * (hub.empty() ? 1 : hub.size())));
   if (!hub.empty())
     HIPCHK(e, hipMemcpy(e->d_hub, hub.data(), sizeof(int64_t) * hub.size(), hipMemcpyHostToDevice));
+  HIPCHK(e, hipMalloc((void**)&e->d_hub_big, sizeof(int64_t) * (hub_big.empty() ? 1 : hub_big.size())));
+  if (!hub_big.empty())
+    HIPCHK(e, hipMemcpy(e->d_hub_big, hub_big.data(), sizeof(int64_t) * hub_big.size(), hipMemcpyHostToDevice));
   e->M = 0;
   e->W = 0;
   e->round = 0;
@@ -411,6 +435,7 @@ int p2pg_reset(p2pg_engine* e) {
   e->round = 0;
   e->done = false;
   e->last_push_e = false;
+  e->prev_aw = e->prev_av = 0;
   for (int i = 0; i < P2PG_KCLASS_N; ++i) {
     e->kms[i] = 0;
     e->klaunch[i] = 0;
@@ -434,6 +459,7 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
   const bool gossip = e->cfg.mode == P2PG_MODE_GOSSIP;
   HIPCHK(e, hipMemsetAsync(s.stats, 0, sizeof(unsigned long long) * STAT_N * STAT_SHARDS, e->stream));
   int rc;
+  bool fused_round = false;
   uint64_t host_new = 0, host_relays = 0, host_av = 0, host_aw = 0, host_wedge = 0, host_degact = 0;
   if (e->round == 0) {
     if ((rc = timed(e, 0, [&] { return launch_zero_rows(s.F[0], e->W, e->d_src, e->M, e->stream); }))) return rc;
@@ -464,8 +490,21 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
   } else if (!gossip) {
     if ((rc = timed(e, 1, [&] { return launch_flood_pull(g, s, p, e->hp, e->stream); }))) return rc;
   } else if (e->last_push_e) {
-    // previous round stored per-edge masks: gather them (pull, no atomics)
-    if ((rc = timed(e, 5, [&] { return launch_gossip_pull(g, s, p, e->hp, e->stream); }))) return rc;
+    // previous round stored per-edge masks: gather them (pull, no atomics).  If this round is
+    // predicted dense as well (the previous round's word density; the prediction only picks
+    // the push form, never the result), the same pass also pushes this round's receipts.
+    const bool dense_pred = e->push_mode == 2 ||
+        (e->push_mode == 0 && e->prev_av > 0 &&
+         (double)e->prev_aw >= e->e_thresh * (double)e->prev_av * (double)e->W);
+    fused_round = s.E[1] != s.E[0] && s.AW[0] && e->W <= 64 && !e->d_gid && dense_pred;
+    if (fused_round) {
+      if ((rc = timed(e, 7, [&] {
+             return launch_gossip_fused(g, s, p, e->hp, e->d_hub_big, e->n_hub_big, e->stream);
+           })))
+        return rc;
+    } else {
+      if ((rc = timed(e, 5, [&] { return launch_gossip_pull(g, s, p, e->hp, e->stream); }))) return rc;
+    }
   } else {
     if ((rc = timed(e, 4, [&] { return launch_gossip_update(g, s, p, e->stream); }))) return rc;
   }
@@ -491,11 +530,13 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
     }
     return P2PG_OK;
   };
-  if (gossip) {
+  if (gossip && fused_round) {
+    e->last_push_e = true;  // the fused launches pushed every source of this round
+  } else if (gossip) {
     // push form for this round's sends: row atomics when the frontier is sparse, whole-row
     // edge-mask stores (+ pull next round) when most words of the active rows are set
     bool use_e = false;
-    if (s.E && !e->d_gid) {  // partitioned gossip pushes by row atomics (ghost rows travel)
+    if (s.E[0] && !e->d_gid) {  // partitioned gossip pushes by row atomics (ghost rows travel)
       if (e->push_mode == 2) {
         use_e = true;
       } else if (e->push_mode == 0) {
@@ -523,7 +564,12 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
     out->deg_active = tot[ST_DEG_ACT];
     out->scatter_words = tot[ST_SCATTER];
     out->touched_words = tot[ST_AUX];
+    out->push_form = !gossip ? P2PG_PUSH_NONE
+                     : fused_round ? P2PG_PUSH_FUSED
+                     : e->last_push_e ? P2PG_PUSH_EDGE : P2PG_PUSH_ATOMIC;
   }
+  e->prev_aw = tot[ST_ACTIVE_W];
+  e->prev_av = tot[ST_ACTIVE_V];
   e->round += 1;
   if (!active && !(e->cfg.flags & P2PG_FLAG_NO_AUTOSTOP)) e->done = true;
   return active ? 1 : 0;

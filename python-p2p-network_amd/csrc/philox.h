@@ -43,9 +43,15 @@ P2PG_HD u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
     const uint64_t p0 = (uint64_t)PHILOX_M0 * c.x;
     const uint64_t p1 = (uint64_t)PHILOX_M1 * c.z;
     u32x4 n;
+#if defined(__HIP_DEVICE_COMPILE__)
+    // gfx950 v_bitop3_b32 (LUT 0x96 = a ^ b ^ c): one VALU op per output word instead of two
+    n.x = (uint32_t)__builtin_amdgcn_bitop3_b32((uint32_t)(p1 >> 32), c.y, k0, 0x96);
+    n.z = (uint32_t)__builtin_amdgcn_bitop3_b32((uint32_t)(p0 >> 32), c.w, k1, 0x96);
+#else
     n.x = (uint32_t)(p1 >> 32) ^ c.y ^ k0;
-    n.y = (uint32_t)p1;
     n.z = (uint32_t)(p0 >> 32) ^ c.w ^ k1;
+#endif
+    n.y = (uint32_t)p1;
     n.w = (uint32_t)p0;
     c = n;
     k0 += PHILOX_W0;

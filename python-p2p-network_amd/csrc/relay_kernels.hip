@@ -138,7 +138,7 @@ __global__ __launch_bounds__(256) void k_pull(DevGraph g, DevState st, RoundPara
   const int64_t V = g.V;
   const int W = st.W;
   const int cur = p.round & 1, prv = cur ^ 1;
-  const uint64_t* __restrict__ Src = GOSSIP ? st.E : st.F[prv];
+  const uint64_t* __restrict__ Src = GOSSIP ? st.E[prv] : st.F[prv];
   uint64_t* __restrict__ Fc = st.F[cur];
   const uint32_t* __restrict__ Ap = st.A[prv];
   const int64_t ntasks = (V + 31) >> 5;
@@ -254,6 +254,7 @@ struct PullStage {
   uint32_t r;       // its source row (flood: v, gossip: the slot itself)
   bool act;         // neighbour active (and its send not lost)
   uint64_t am;      // packed E rows: the neighbour's active-word mask
+  uint32_t rv;      // fused gossip: receiver slot rev[j] of this lane's connection
 };
 
 // Word `lane` of a source row.  Packed E rows (gossip, st.AW) hold only the sender's active
@@ -284,7 +285,7 @@ __global__ __launch_bounds__(256, P2PG_PULL_WAVES) void k_pull1(DevGraph g, DevS
   const int64_t V = g.V;
   const int W = st.W;
   const int cur = p.round & 1, prv = cur ^ 1;
-  const uint64_t* __restrict__ Src = GOSSIP ? st.E : st.F[prv];
+  const uint64_t* __restrict__ Src = GOSSIP ? st.E[prv] : st.F[prv];
   uint64_t* __restrict__ Fc = st.F[cur];
   const uint32_t* __restrict__ Ap = st.A[prv];
   const uint64_t* __restrict__ AWp = GOSSIP ? st.AW[prv] : nullptr;
@@ -450,7 +451,7 @@ __global__ __launch_bounds__(256) void k_pull_hub_partial(DevGraph g, DevState s
   const int wib = wave_in_block();
   const int W = st.W;
   const int prv = (p.round & 1) ^ 1;
-  const uint64_t* __restrict__ Src = GOSSIP ? st.E : st.F[prv];
+  const uint64_t* __restrict__ Src = GOSSIP ? st.E[prv] : st.F[prv];
   const uint32_t* __restrict__ Ap = st.A[prv];
   const uint64_t* __restrict__ AWp = GOSSIP ? st.AW[prv] : nullptr;
   const bool packed = GOSSIP && AWp != nullptr;
@@ -634,6 +635,13 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
+// LDS of one scatter wave: a GCHUNK x 64-word mask table (two 32-bit halves per word, so
+// 32-bit LDS atomics) and the compacted list of active (word, bit) entries.
+struct ScatterLds {
+  uint32_t tbl[GCHUNK][2][64];
+  uint16_t lst[GLIST];
+};
+
 // Gossip, round r >= 0: every first receipt (v, m) of round r is pushed to k Philox-chosen
 // neighbours.  One wave per (source, GCHUNK-neighbour chunk):
 //   1. the row slice's active bits are compacted into an LDS list (prefix sum of popcounts),
@@ -644,39 +652,42 @@ __device__ __forceinline__ void wave_lds_sync() {
 //   3. flush, lane = word: every (target, word) mask leaves as part of one 512 B row access --
 //      STORE_E = false (sparse rounds): row atomicOr into the target's next row + T bit;
 //      STORE_E = true  (dense rounds):  plain store of the whole row (zeros included) into
-//      E[rev(slot)], the receiver's own slot of the connection, which the next round's
-//      k_pull1<GOSSIP> then streams contiguously per receiver.
-// Every per-source value (row offsets, global id, neighbour ids) is a scalar load or a lane
-// of a prefetched register: a vector load inside the loop would make the wave wait (vmcnt)
-// for its own in-flight row stores / atomics before every Philox batch.
+//      E[r&1][rev(slot)], the receiver's own slot of the connection, which the next round's
+//      pull then streams contiguously per receiver.
+// One (source v, neighbour chunk, row slice): f = this lane's frontier word, nbr = lane j's
+// neighbour nb + j is lane nbr0 + j of nbr -- its receiver slot (STORE_E) or its local id
+// (row atomics).  Every
+// per-source value is a scalar load or a lane of a prefetched register: a vector load here
+// would make the wave wait (vmcnt) for its own in-flight row stores / atomics.
 template <bool CHURN, int K, bool STORE_E>
-__global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st, RoundParams p,
-                                                        const int64_t* __restrict__ hub_items,
-                                                        int64_t n_hub) {
-  __shared__ uint32_t tbl[WPB][GCHUNK][2][64];
-  __shared__ uint16_t lst[WPB][GLIST];
-  const int lane = threadIdx.x & 63;
-  const int wib = wave_in_block();
-  const int64_t V = g.V;
+__device__ __forceinline__ void scatter_row(const DevGraph& g, const DevState& st,
+                                            const RoundParams& p, ScatterLds& L, int lane,
+                                            int64_t v, int64_t rb, int64_t deg, int chunk,
+                                            int sl, uint64_t f, uint32_t nbr, int nbr0,
+                                            uint64_t* c) {
   const int W = st.W;
   const int cur = p.round & 1, nxt = cur ^ 1;
-  const uint64_t* __restrict__ Fc = st.F[cur];
   uint64_t* __restrict__ nx = st.next[nxt];
   uint32_t* __restrict__ Tn = st.T[nxt];
-  const int64_t nwords = (V + 31) >> 5;
-  const int64_t ntasks = nwords + n_hub;
-  const int nslices = (W + 63) >> 6;
+  uint64_t* __restrict__ Eo = st.E[cur];
   const int k = K > 0 ? K : p.fanout;
-  uint64_t c[STAT_N] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int nb = chunk * GCHUNK;
+  const int nn = (int)(deg - nb < GCHUNK ? deg - nb : GCHUNK);
+  const bool all = deg <= k;
+  const int w = sl * 64 + lane;
+  const bool valid = w < W;
+  const uint64_t fam = __ballot(f != 0ull);  // active words of this slice
+  const bool anyf = fam != 0ull;
+  if (!anyf && !STORE_E) return;
+  const uint32_t gv = gidx_s(g, v);
 
   // Philox + Floyd for list entries [0, n) of this wave, picks ORed into the LDS table.
-  auto pick_batch = [&](auto check_v, uint32_t n, int sl, uint32_t gv, int64_t deg, int nb,
-                        int nn) {
+  auto pick_batch = [&](auto check_v, uint32_t n) {
     constexpr bool CHECK = decltype(check_v)::value;
-    auto one = [&](uint32_t e, bool ok) {
+    auto one = [&](uint32_t e) {
       const uint32_t wl = e >> 6, bit = e & 63u;
       const uint32_t mg = p.msg_base + (uint32_t)((sl * 64 + (int)wl) * 64) + bit;
-      uint32_t* const col = &tbl[wib][0][bit >> 5][wl];
+      uint32_t* const col = &L.tbl[0][bit >> 5][wl];
       const uint32_t mb = 1u << (bit & 31u);
       uint32_t pk[K > 0 ? K : 1];
       gossip_picks_t<(K > 0 ? K : 1)>((uint32_t)p.round, gv, mg, (uint32_t)deg, p.gseed_lo,
@@ -684,125 +695,128 @@ __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st,
 #pragma unroll
       for (int q = 0; q < (K > 0 ? K : 1); ++q) {
         const uint32_t jj = pk[q] - (uint32_t)nb;
-        if (ok && (!CHECK || jj < (uint32_t)nn)) atomicOr(col + jj * 128u, mb);
+        if (!CHECK || jj < (uint32_t)nn) atomicOr(col + jj * 128u, mb);
       }
     };
     // the next batch's list entry is read before this batch's Philox (hides the LDS trip)
-    uint32_t en = (uint32_t)lane < n ? lst[wib][lane] : 0u;
+    uint32_t en = (uint32_t)lane < n ? L.lst[lane] : 0u;
     for (uint32_t i = lane; i < n; i += 64) {
       const uint32_t e = en;
-      en = i + 64 < n ? lst[wib][i + 64] : 0u;
-      one(e, true);
+      en = i + 64 < n ? L.lst[i + 64] : 0u;
+      one(e);
     }
   };
 
-  // One (source v, neighbour chunk, row slice): f = this lane's frontier word, nbr = lane j's
-  // neighbour nb + j -- its receiver slot (STORE_E) or its local id (row atomics).
-  auto body = [&](int64_t v, int64_t rb, int64_t deg, int chunk, int sl, uint64_t f,
-                  uint32_t nbr) {
-    const int nb = chunk * GCHUNK;
-    const int nn = (int)(deg - nb < GCHUNK ? deg - nb : GCHUNK);
-    const bool all = deg <= k;
-    const int w = sl * 64 + lane;
-    const bool valid = w < W;
-    const uint64_t fam = __ballot(f != 0ull);  // active words of this slice
-    const bool anyf = fam != 0ull;
-    if (!anyf && !STORE_E) return;
-    const uint32_t gv = gidx_s(g, v);
-    if (anyf && !all) {
-      for (int j = 0; j < nn; ++j) {
-        tbl[wib][j][0][lane] = 0u;
-        tbl[wib][j][1][lane] = 0u;
-      }
-      // rank-major compaction: list = every word's 1st set bit, then every word's 2nd set
-      // bit, ... so a 64-entry batch covers ~64 distinct words (distinct LDS banks), while
-      // every lane still gets equal Philox work
-      const uint32_t cnt = (uint32_t)__popcll(f);
-      const uint32_t maxc = wave_reduce_u32<true>(cnt);
-      const uint32_t total = wave_reduce_u32<false>(cnt);
-      for (uint32_t lb = 0; lb < total; lb += GLIST) {
-        uint64_t ff = f;
-        uint32_t base = 0;
-        for (uint32_t kr = 0; kr < maxc; ++kr) {
-          const bool has = cnt > kr;
-          const uint64_t mk = __ballot(has);
-          if (has) {
-            const uint32_t pos =
-                base + __builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32),
-                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
-            const int bit = __builtin_ctzll(ff);
-            ff &= ff - 1ull;
-            if (pos >= lb && pos < lb + GLIST) lst[wib][pos - lb] = (uint16_t)((lane << 6) | bit);
-          }
-          base += (uint32_t)__popcll(mk);
-        }
-        wave_lds_sync();
-        const uint32_t n = total - lb < (uint32_t)GLIST ? total - lb : (uint32_t)GLIST;
-        if constexpr (K > 0) {
-          // a source whose whole adjacency is this chunk needs no range check on its picks
-          if (nb == 0 && nn == (int)deg)
-            pick_batch(std::false_type{}, n, sl, gv, deg, nb, nn);
-          else
-            pick_batch(std::true_type{}, n, sl, gv, deg, nb, nn);
-        } else {
-          for (uint32_t i = lane; i < n; i += 64) {
-            const uint32_t e = lst[wib][i];
-            const uint32_t wl = e >> 6, bit = e & 63u;
-            const uint32_t mg = p.msg_base + (uint32_t)((sl * 64 + (int)wl) * 64) + bit;
-            uint32_t* const col = &tbl[wib][0][bit >> 5][wl];
-            const uint32_t mb = 1u << (bit & 31u);
-            uint32_t pk[16];
-            gossip_picks((uint32_t)p.round, gv, mg, (uint32_t)deg, k, p.gseed_lo, p.gseed_hi,
-                         pk);
-            for (int q = 0; q < k; ++q) {
-              const uint32_t jj = pk[q] - (uint32_t)nb;
-              if (jj < (uint32_t)nn) atomicOr(col + jj * 128u, mb);
-            }
-          }
-        }
-        wave_lds_sync();
-      }
-    }
-    const bool use_tbl = anyf && !all;
-    auto tbl_row = [&](int j) -> uint64_t {
-      return ((uint64_t)tbl[wib][j][1][lane] << 32) | tbl[wib][j][0][lane];
-    };
-    uint64_t xn = use_tbl && nn > 0 ? tbl_row(0) : 0ull;
+  if (anyf && !all) {
     for (int j = 0; j < nn; ++j) {
-      const uint64_t x = all ? f : xn;  // row j; row j + 1 is read before row j is stored
-      if (use_tbl && j + 1 < nn) xn = tbl_row(j + 1);
-      const uint64_t bal = __ballot(x != 0ull);
-      const uint32_t nj = (uint32_t)__builtin_amdgcn_readlane((int)nbr, j);
-      if (STORE_E) {
-        bool dropped = false;
-        if (CHURN && bal)
-          dropped = churn_dropped((uint32_t)p.round, gv, gidx_s(g, ldc(g.colidx + rb + nb + j)),
-                                  p.churn_thr, p.cseed_lo, p.cseed_hi);
-        // receiver-major: the row lands in the RECEIVER's slot for this connection, so the
-        // pull streams its own contiguous slot range; packed: only the active words, in order
-#ifdef P2PG_DIAG_NO_ESTORE  // diagnostic build only (wrong results): the stores' cost
-        if (p.round < 0)
-#endif
-        if (st.AW[cur]) {
-          if (f) st.E[(int64_t)nj * W + __popcll(fam & ((1ull << lane) - 1ull))] = dropped ? 0ull : x;
-        } else if (valid) {
-          st.E[(int64_t)nj * W + w] = dropped ? 0ull : x;
+      L.tbl[j][0][lane] = 0u;
+      L.tbl[j][1][lane] = 0u;
+    }
+    // rank-major compaction: list = every word's 1st set bit, then every word's 2nd set
+    // bit, ... so a 64-entry batch covers ~64 distinct words (distinct LDS banks), while
+    // every lane still gets equal Philox work
+    const uint32_t cnt = (uint32_t)__popcll(f);
+    const uint32_t maxc = wave_reduce_u32<true>(cnt);
+    const uint32_t total = wave_reduce_u32<false>(cnt);
+    for (uint32_t lb = 0; lb < total; lb += GLIST) {
+      uint64_t ff = f;
+      uint32_t base = 0;
+      for (uint32_t kr = 0; kr < maxc; ++kr) {
+        const bool has = cnt > kr;
+        const uint64_t mk = __ballot(has);
+        if (has) {
+          const uint32_t pos =
+              base + __builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32),
+                                               __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
+          const int bit = __builtin_ctzll(ff);
+          ff &= ff - 1ull;
+          if (pos >= lb && pos < lb + GLIST) L.lst[pos - lb] = (uint16_t)((lane << 6) | bit);
         }
-        if (!dropped && lane == 0) c[ST_SCATTER] += (uint64_t)__popcll(bal);
+        base += (uint32_t)__popcll(mk);
+      }
+      wave_lds_sync();
+      const uint32_t n = total - lb < (uint32_t)GLIST ? total - lb : (uint32_t)GLIST;
+      if constexpr (K > 0) {
+        // a source whose whole adjacency is this chunk needs no range check on its picks
+        if (nb == 0 && nn == (int)deg)
+          pick_batch(std::false_type{}, n);
+        else
+          pick_batch(std::true_type{}, n);
       } else {
-        if (!bal) continue;
-        const int64_t u = (int64_t)nj;
-        if (CHURN && churn_dropped((uint32_t)p.round, gv, gidx_s(g, u), p.churn_thr,
-                                   p.cseed_lo, p.cseed_hi))
-          continue;
-        if (x) atomicOr((unsigned long long*)&nx[u * W + w], (unsigned long long)x);
-        if (lane == 0) {
-          atomicOr(&Tn[u >> 5], 1u << (u & 31));
-          c[ST_SCATTER] += (uint64_t)__popcll(bal);
+        for (uint32_t i = lane; i < n; i += 64) {
+          const uint32_t e = L.lst[i];
+          const uint32_t wl = e >> 6, bit = e & 63u;
+          const uint32_t mg = p.msg_base + (uint32_t)((sl * 64 + (int)wl) * 64) + bit;
+          uint32_t* const col = &L.tbl[0][bit >> 5][wl];
+          const uint32_t mb = 1u << (bit & 31u);
+          uint32_t pk[16];
+          gossip_picks((uint32_t)p.round, gv, mg, (uint32_t)deg, k, p.gseed_lo, p.gseed_hi, pk);
+          for (int q = 0; q < k; ++q) {
+            const uint32_t jj = pk[q] - (uint32_t)nb;
+            if (jj < (uint32_t)nn) atomicOr(col + jj * 128u, mb);
+          }
         }
       }
+      wave_lds_sync();
     }
+  }
+  const bool use_tbl = anyf && !all;
+  auto tbl_row = [&](int j) -> uint64_t {
+    return ((uint64_t)L.tbl[j][1][lane] << 32) | L.tbl[j][0][lane];
   };
+  uint64_t xn = use_tbl && nn > 0 ? tbl_row(0) : 0ull;
+  for (int j = 0; j < nn; ++j) {
+    const uint64_t x = all ? f : xn;  // row j; row j + 1 is read before row j is stored
+    if (use_tbl && j + 1 < nn) xn = tbl_row(j + 1);
+    const uint64_t bal = __ballot(x != 0ull);
+    const uint32_t nj = (uint32_t)__builtin_amdgcn_readlane((int)nbr, nbr0 + j);
+    if (STORE_E) {
+      bool dropped = false;
+      if (CHURN && bal)
+        dropped = churn_dropped((uint32_t)p.round, gv, gidx_s(g, ldc(g.colidx + rb + nb + j)),
+                                p.churn_thr, p.cseed_lo, p.cseed_hi);
+      // receiver-major: the row lands in the RECEIVER's slot for this connection, so the
+      // pull streams its own contiguous slot range; packed: only the active words, in order
+      if (st.AW[cur]) {
+        if (f) Eo[(int64_t)nj * W + __popcll(fam & ((1ull << lane) - 1ull))] = dropped ? 0ull : x;
+      } else if (valid) {
+        Eo[(int64_t)nj * W + w] = dropped ? 0ull : x;
+      }
+      if (!dropped && lane == 0) c[ST_SCATTER] += (uint64_t)__popcll(bal);
+    } else {
+      if (!bal) continue;
+      const int64_t u = (int64_t)nj;
+      if (CHURN && churn_dropped((uint32_t)p.round, gv, gidx_s(g, u), p.churn_thr,
+                                 p.cseed_lo, p.cseed_hi))
+        continue;
+      if (x) atomicOr((unsigned long long*)&nx[u * W + w], (unsigned long long)x);
+      if (lane == 0) {
+        atomicOr(&Tn[u >> 5], 1u << (u & 31));
+        c[ST_SCATTER] += (uint64_t)__popcll(bal);
+      }
+    }
+  }
+}
+
+// The scatter launch: tasks [task0, nwords) are 32-peer bitmap words (sources with deg <=
+// GCHUNK), tasks [nwords, nwords + n_hub) are (wide source, chunk) items.  task0 = nwords
+// runs the wide sources only (after k_gossip_fused has scattered the narrow ones).
+template <bool CHURN, int K, bool STORE_E>
+__global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st, RoundParams p,
+                                                        const int64_t* __restrict__ hub_items,
+                                                        int64_t n_hub, int64_t task0) {
+  __shared__ ScatterLds lds[WPB];
+  const int lane = threadIdx.x & 63;
+  const int wib = wave_in_block();
+  ScatterLds& L = lds[wib];
+  const int64_t V = g.V;
+  const int W = st.W;
+  const int cur = p.round & 1;
+  const uint64_t* __restrict__ Fc = st.F[cur];
+  const int64_t nwords = (V + 31) >> 5;
+  const int64_t ntasks = nwords + n_hub;
+  const int nslices = (W + 63) >> 6;
+  uint64_t c[STAT_N] = {0, 0, 0, 0, 0, 0, 0, 0};
 
   // lane j's neighbour datum for the chunk starting at slot rb + nb
   auto load_nbr = [&](int64_t rb, int nn) -> uint32_t {
@@ -810,7 +824,7 @@ __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st,
     return STORE_E ? g.rev[rb + lane] : (uint32_t)g.colidx[rb + lane];
   };
 
-  for (int64_t task = (int64_t)blockIdx.x * WPB + wib; task < ntasks;
+  for (int64_t task = task0 + (int64_t)blockIdx.x * WPB + wib; task < ntasks;
        task += (int64_t)gridDim.x * WPB) {
     if (task < nwords && nslices == 1) {
       // pipelined: row offsets of the 32 peers in one load; the next active peer's frontier
@@ -847,7 +861,8 @@ __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st,
           if (lane < W) f2 = Fc[(base + b2) * W + lane];
           rv2 = load_nbr(rb2, (int)deg2);
         }
-        body(base + b1, rb1, deg1, 0, 0, f1, rv1);
+        scatter_row<CHURN, K, STORE_E>(g, st, p, L, lane, base + b1, rb1, deg1, 0, 0, f1, rv1, 0,
+                                       c);
         b1 = b2;
         rb1 = rb2;
         deg1 = deg2;
@@ -882,8 +897,184 @@ __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st,
       for (int sl = 0; sl < nslices; ++sl) {
         const int w = sl * 64 + lane;
         const uint64_t f = w < W ? Fc[v * W + w] : 0ull;
-        body(v, rb, deg, chunk, sl, f, rv);
+        scatter_row<CHURN, K, STORE_E>(g, st, p, L, lane, v, rb, deg, chunk, sl, f, rv, 0, c);
       }
+    }
+  }
+  flush_stats(st.stats, c, lane);
+}
+
+// Gossip dense round r >= 1 after a dense round r-1: the pull of round r (k_pull1<false,
+// true>: arrivals = packed E[(r-1)&1] rows of the active neighbours) and, for every peer with
+// a first receipt, its own round-r pushes (scatter_row<STORE_E> into E[r&1]) in the same
+// pass.  The new frontier row goes straight from registers into the picks (no HBM round trip,
+// no second pass over the peers), and the Philox work of one target overlaps the gathers of
+// the next two, which are already in flight.  Hubs (deg > HUB_T) are pulled by k_pull_hub_*
+// and pushed by a chunk-item scatter launch over the hubs only.
+template <bool CHURN, int K>
+__global__ __launch_bounds__(256) void k_gossip_fused(DevGraph g, DevState st, RoundParams p) {
+  __shared__ ScatterLds lds[WPB];
+  const int lane = threadIdx.x & 63;
+  const int wib = wave_in_block();
+  const int64_t V = g.V;
+  const int W = st.W;
+  const int cur = p.round & 1, prv = cur ^ 1;
+  const uint64_t* __restrict__ Src = st.E[prv];
+  uint64_t* __restrict__ Fc = st.F[cur];
+  const uint32_t* __restrict__ Ap = st.A[prv];
+  const uint64_t* __restrict__ AWp = st.AW[prv];
+  const int64_t ntasks = (V + 31) >> 5;
+  const bool valid = lane < W;
+  const uint64_t fm = valid ? full_mask(lane, W, st.M) : 0ull;
+  uint64_t c[STAT_N] = {0, 0, 0, 0, 0, 0, 0, 0};
+
+  for (int64_t task = (int64_t)blockIdx.x * WPB + wib; task < ntasks;
+       task += (int64_t)gridDim.x * WPB) {
+    const int64_t u0 = task << 5;
+    const uint32_t sat0 = st.S[task];
+    uint32_t todo = ~sat0;
+    if (g.H) todo &= ~g.H[task];  // hubs: k_pull_hub_* items
+    if (V - u0 < 32) todo &= (1u << (V - u0)) - 1u;
+    if (!todo) {
+      if (lane == 0) st.A[cur][task] = 0u;
+      continue;
+    }
+    int64_t rp = 0;
+    if (lane <= 32 && u0 + lane <= V) rp = g.rowptr[u0 + lane];
+
+    auto issue = [&](PullStage& q, int b) {
+      q.b = b;
+      q.act = false;
+      q.v = 0;
+      q.r = 0;
+      q.rv = 0;
+      q.s = 0;
+      if (b < 0) return;
+      q.beg = readlane64(rp, b);
+      q.end = readlane64(rp, b + 1);
+      if (valid) q.s = st.seen[(u0 + b) * W + lane];
+      const int64_t j = q.beg + lane;
+      if (j < q.end) {
+        q.v = g.colidx[j];
+        q.r = (uint32_t)j;
+        q.rv = g.rev[j];
+      }
+    };
+    auto activity = [&](PullStage& q) {
+      if (q.b < 0) return;
+      const int64_t j = q.beg + lane;
+      q.am = 0;
+      bool a = false;
+      if (j < q.end) {
+        q.am = AWp[q.v];
+        a = bit_test(Ap, q.v);
+      }
+      q.act = a;
+    };
+    auto next_bit = [](uint32_t& t) -> int {
+      if (!t) return -1;
+      const int b = __builtin_ctz(t);
+      t &= t - 1u;
+      return b;
+    };
+
+    uint32_t rest = todo;
+    PullStage s1, s2, s3;
+    issue(s1, next_bit(rest));
+    issue(s2, next_bit(rest));
+    activity(s1);
+    uint32_t aw = 0, sat = sat0;
+    while (s1.b >= 0) {
+      issue(s3, next_bit(rest));
+      activity(s2);
+      const int64_t u = u0 + s1.b;
+      const uint64_t deg = (uint64_t)(s1.end - s1.beg);
+      const uint64_t need = fm & ~s1.s;
+      uint64_t acc = 0;
+      if (__ballot(need != 0ull)) {
+        uint64_t m = __ballot(s1.act);
+        uint32_t srow = s1.r;
+        uint64_t sam = s1.am;
+        int64_t cb = s1.beg;
+        for (;;) {
+          while (m) {
+            uint32_t sv[8];
+            uint64_t am[8];
+            bool ok[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              ok[k] = m != 0ull;
+              am[k] = 0ull;
+              if (m) {
+                const int idx = __builtin_ctzll(m);
+                m &= m - 1ull;
+                sv[k] = (uint32_t)__builtin_amdgcn_readlane((int)srow, idx);
+                am[k] = (uint64_t)readlane64((int64_t)sam, idx);
+              } else {
+                sv[k] = 0u;
+              }
+            }
+            uint64_t x[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+              x[k] = src_word(Src, sv[k], W, lane, true, am[k], ok[k] && need);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc |= x[k];
+          }
+          cb += 64;
+          if (cb >= s1.end) break;
+          const int64_t j = cb + lane;  // further chunks of a wide row: serial
+          bool a = false;
+          srow = 0;
+          sam = 0;
+          if (j < s1.end) {
+            const int32_t v = g.colidx[j];
+            srow = (uint32_t)j;
+            a = bit_test(Ap, v);
+            if (a) sam = AWp[v];
+          }
+          m = __ballot(a);
+        }
+      }
+      const uint64_t nw = acc & need;
+      const uint64_t wm = __ballot(nw != 0ull);
+      if (nw) {
+        st.seen[u * W + lane] = s1.s | nw;
+        const uint64_t pc = (uint64_t)__popcll(nw);
+        const uint64_t per_bit = deg < (uint64_t)p.fanout ? deg : (uint64_t)p.fanout;
+        c[ST_NEW] += pc;
+        c[ST_RELAYS] += pc * per_bit;
+        c[ST_ACTIVE_W] += 1;
+        c[ST_WEDGES] += deg;
+      }
+      if (wm) {
+        if (valid) Fc[u * W + lane] = nw;
+        aw |= 1u << s1.b;
+        if (lane == 0) {
+          st.AW[cur][u] = wm;
+          c[ST_ACTIVE_V] += 1;
+          c[ST_DEG_ACT] += deg;
+        }
+        // this round's pushes, GCHUNK connections at a time (s1.rv holds the receiver slots
+        // of the first 64; wider rows load the next 64 every 4 chunks)
+        uint32_t rvb = s1.rv;
+        for (int ch = 0; (int64_t)ch * GCHUNK < (int64_t)deg; ++ch) {
+          const int off = (ch * GCHUNK) & 63;
+          if (ch > 0 && off == 0) {
+            const int64_t j = s1.beg + (int64_t)ch * GCHUNK + lane;
+            rvb = j < s1.end ? g.rev[j] : 0u;
+          }
+          scatter_row<CHURN, K, true>(g, st, p, lds[wib], lane, u, s1.beg, (int64_t)deg, ch, 0,
+                                      nw, rvb, off, c);
+        }
+      }
+      if (!__ballot(valid && (s1.s | nw) != fm)) sat |= 1u << s1.b;
+      s1 = s2;
+      s2 = s3;
+    }
+    if (lane == 0) {
+      st.A[cur][task] = aw;
+      if (sat != sat0) st.S[task] = sat;
     }
   }
   flush_stats(st.stats, c, lane);
@@ -1116,10 +1307,11 @@ hipError_t launch_gossip_update(const DevGraph& g, const DevState& st, const Rou
 
 template <bool SE>
 void scatter_dispatch(int grid, const DevGraph& g, const DevState& st, const RoundParams& p,
-                      const int64_t* hub_items, int64_t n_hub_items, hipStream_t s) {
+                      const int64_t* hub_items, int64_t n_hub_items, int64_t task0,
+                      hipStream_t s) {
 #define P2PG_SCATTER(CH, KK)                                                                 \
   hipLaunchKernelGGL((k_gossip_scatter<CH, KK, SE>), dim3(grid), dim3(256), 0, s, g, st, p,  \
-                     hub_items, n_hub_items)
+                     hub_items, n_hub_items, task0)
   const bool ch = p.churn_thr != 0;
   switch (p.fanout) {
     case 1: if (ch) P2PG_SCATTER(true, 1); else P2PG_SCATTER(false, 1); break;
@@ -1136,9 +1328,38 @@ hipError_t launch_gossip_scatter(const DevGraph& g, const DevState& st, const Ro
                                  hipStream_t s) {
   const int grid = grid_tasks(((g.V + 31) >> 5) + n_hub_items);
   if (store_e)
-    scatter_dispatch<true>(grid, g, st, p, hub_items, n_hub_items, s);
+    scatter_dispatch<true>(grid, g, st, p, hub_items, n_hub_items, 0, s);
   else
-    scatter_dispatch<false>(grid, g, st, p, hub_items, n_hub_items, s);
+    scatter_dispatch<false>(grid, g, st, p, hub_items, n_hub_items, 0, s);
+  return hipGetLastError();
+}
+
+hipError_t launch_gossip_fused(const DevGraph& g, const DevState& st, const RoundParams& p,
+                               const HubPlan& hp, const int64_t* big_items, int64_t n_big,
+                               hipStream_t s) {
+  if (st.W > 64 || !st.AW[0] || st.E[0] == st.E[1]) return hipErrorInvalidValue;
+  const int grid = grid_tasks((g.V + 31) >> 5);
+  if (hp.n_items)
+    hipLaunchKernelGGL((k_pull_hub_partial<false, true>), dim3(grid_tasks(hp.n_items)),
+                       dim3(256), 0, s, g, st, p, hp);
+#define P2PG_FUSED(CH, KK) \
+  hipLaunchKernelGGL((k_gossip_fused<CH, KK>), dim3(grid), dim3(256), 0, s, g, st, p)
+  const bool ch = p.churn_thr != 0;
+  switch (p.fanout) {
+    case 1: if (ch) P2PG_FUSED(true, 1); else P2PG_FUSED(false, 1); break;
+    case 2: if (ch) P2PG_FUSED(true, 2); else P2PG_FUSED(false, 2); break;
+    case 3: if (ch) P2PG_FUSED(true, 3); else P2PG_FUSED(false, 3); break;
+    case 4: if (ch) P2PG_FUSED(true, 4); else P2PG_FUSED(false, 4); break;
+    default: if (ch) P2PG_FUSED(true, 0); else P2PG_FUSED(false, 0); break;
+  }
+#undef P2PG_FUSED
+  if (hp.n_hubs)
+    hipLaunchKernelGGL((k_pull_hub_finalize<true>), dim3(grid_tasks(hp.n_hubs)), dim3(256), 0,
+                       s, g, st, p, hp);
+  if (n_big) {
+    const int64_t nwords = (g.V + 31) >> 5;
+    scatter_dispatch<true>(grid_tasks(n_big), g, st, p, big_items, n_big, nwords, s);
+  }
   return hipGetLastError();
 }
 

@@ -59,6 +59,8 @@ class RoundStatsC(ctypes.Structure):
         ("deg_active", ctypes.c_uint64),
         ("scatter_words", ctypes.c_uint64),
         ("touched_words", ctypes.c_uint64),
+        ("push_form", ctypes.c_int32),
+        ("reserved_", ctypes.c_int32),
     ]
 
 

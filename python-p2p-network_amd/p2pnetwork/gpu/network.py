@@ -26,6 +26,9 @@ import numpy as np
 from . import _lib
 from .graph import PeerGraph
 
+# p2pg_round_stats.push_form (include/p2pgpu.h P2PG_PUSH_*)
+PUSH_FORMS = ("none", "atomic", "edge", "fused")
+
 STAT_FIELDS = ("round", "active", "new_deliveries", "relays", "active_vertices", "active_words",
                "wedges", "deg_active", "scatter_words", "touched_words")
 
@@ -42,10 +45,11 @@ class RoundStats:
     deg_active: int
     scatter_words: int
     touched_words: int
+    push_form: int = 0  # gossip: how this round's pushes left (PUSH_FORMS); not a result
 
     @classmethod
     def from_c(cls, s):
-        return cls(*(int(getattr(s, f)) for f in STAT_FIELDS))
+        return cls(*(int(getattr(s, f)) for f in STAT_FIELDS), push_form=int(s.push_form))
 
     def as_dict(self):
         return {f: getattr(self, f) for f in STAT_FIELDS}
@@ -239,7 +243,7 @@ class GraphNetwork:
         return hop, par
 
     KERNEL_CLASSES = ("seed", "flood_pull", "gossip_scatter_atomic", "record", "gossip_update",
-                      "gossip_pull", "gossip_scatter_store", "reserved")
+                      "gossip_pull", "gossip_scatter_store", "gossip_fused")
 
     def kernel_times(self):
         """Summed device ms and launch counts per kernel class since the last reset (needs

@@ -281,17 +281,23 @@ def test_gpu_gossip_push_forms_match_golden(name, push, monkeypatch):
     assert_rounds_equal(rounds, ora.rounds)
 
 
-@pytest.mark.parametrize("push", ["atomic", "store"])
+@pytest.mark.parametrize("push", ["atomic", "store", "store_unfused"])
 @pytest.mark.parametrize("kind,p,M,thr,fanout", [
     ("hub", dict(V=1500, m=3, star=1100), 64, 0, 3),
+    ("hub", dict(V=1500, m=3, star=300), 256, 0, 3),
+    ("hub", dict(V=1500, m=3, star=300), 128, 400_000_000, 4),
     ("ba", dict(V=600, m=3), 64, 0, 3),
     ("ws", dict(V=500, k=6, b=0.2), 200, 300_000_000, 2),
     ("ba", dict(V=150, m=20), 4160, 0, 3),
     ("gnp", dict(V=300, k=5.0), 130, 0, 7),
 ])
 def test_gpu_gossip_push_forms_match_oracle(kind, p, M, thr, fanout, push, monkeypatch):
+    """Row atomics, edge stores with fused pull+scatter rounds (k_gossip_fused: every round
+    after the first when W <= 64; narrow, chunked (deg > GCHUNK, > 64) and hub sources), and
+    edge stores with separate pull / scatter passes all equal the oracle bit for bit."""
     from p2pnetwork.gpu import make_sources
-    monkeypatch.setenv("P2PG_GOSSIP_PUSH", push)
+    monkeypatch.setenv("P2PG_GOSSIP_PUSH", push.split("_")[0])
+    monkeypatch.setenv("P2PG_FUSED", "0" if push == "store_unfused" else "1")
     seed = zlib.crc32(repr((kind, M, thr, fanout)).encode()) & 0xFFFF
     g = make_graph(kind, p, seed)
     src = make_sources(g.V, M, seed=seed + 3)
@@ -299,6 +305,13 @@ def test_gpu_gossip_push_forms_match_oracle(kind, p, M, thr, fanout, push, monke
         net.broadcast(src)
         rounds = net.run()
         hop, parent = net.hop_parent()
+    forms = [r.push_form for r in rounds if r.new_deliveries]
+    if push == "store" and M <= 4096:
+        assert forms[0] == 2 and all(f == 3 for f in forms[1:]), forms
+    elif push.startswith("store"):
+        assert all(f == 2 for f in forms), forms
+    else:
+        assert all(f == 1 for f in forms), forms
     ora = oracle_for(g.rowptr, g.colidx, src, "gossip", fanout, 99 + seed, thr, 5 + seed)
     np.testing.assert_array_equal(hop, ora.hop)
     np.testing.assert_array_equal(parent, ora.parent)

@@ -49,6 +49,8 @@ def calib(d):
 def cls(name):
     """rocprof kernel name -> bench.py timer class (include/p2pgpu.h P2PG_KCLASS_N)."""
     tmpl = name.split("<", 1)[1].split(">(")[0] if "<" in name else ""
+    if "k_gossip_fused" in name:
+        return "gossip_fused"
     if "k_gossip_scatter" in name:
         return "gossip_scatter_store" if tmpl.rstrip().endswith("true") else "gossip_scatter_atomic"
     if "k_pull" in name:
