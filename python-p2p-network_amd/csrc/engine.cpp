@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <numeric>
@@ -116,6 +117,17 @@ void free_state(p2pg_engine* e) {
   for (int i = 0; i < 2; ++i) dfree(s.E[i]);
   for (int i = 0; i < 2; ++i) dfree(s.AW[i]);
   dfree(s.stats);
+#ifdef P2PG_PROF
+  if (s.prof) {
+    unsigned long long h[16];
+    if (hipMemcpy(h, s.prof, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess) {
+      fprintf(stderr, "P2PG_PROF");
+      for (int i = 0; i < 16; ++i) fprintf(stderr, " %llu", h[i]);
+      fprintf(stderr, "\n");
+    }
+  }
+  dfree(s.prof);
+#endif
   dfree(e->d_src);
   e->have_state = false;
 }
@@ -248,6 +260,10 @@ int alloc_state(p2pg_engine* e) {
     if ((rc = A((void**)&s.parent, hb))) return rc;
   }
   if ((rc = A((void**)&s.stats, sizeof(unsigned long long) * STAT_N * STAT_SHARDS))) return rc;
+#ifdef P2PG_PROF
+  if ((rc = A((void**)&s.prof, sizeof(unsigned long long) * 16))) return rc;
+  HIPCHK(e, hipMemset(s.prof, 0, sizeof(unsigned long long) * 16));
+#endif
   if ((rc = A((void**)&e->d_src, sizeof(int32_t) * (e->M ? e->M : 1)))) return rc;
   e->have_state = true;
   return P2PG_OK;

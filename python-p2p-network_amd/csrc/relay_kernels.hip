@@ -22,6 +22,8 @@
 // so stats need few atomics.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 #include "internal.h"
@@ -252,7 +254,9 @@ struct PullStage {
   uint64_t s;       // this lane's seen word
   int32_t v;        // this lane's neighbour (first chunk)
   uint32_t r;       // its source row (flood: v, gossip: the slot itself)
-  bool act;         // neighbour active (and its send not lost)
+  bool act;         // neighbour active (and its send not lost); set by resolve() at use
+  uint32_t aword;   // the neighbour's word of the activity bitmap, as loaded
+  uint64_t mr;      // fused: active slots (of the first 64) not yet gathered
   uint64_t am;      // packed E rows: the neighbour's active-word mask
   uint32_t rv;      // fused gossip: receiver slot rev[j] of this lane's connection
 };
@@ -325,19 +329,25 @@ __global__ __launch_bounds__(256, P2PG_PULL_WAVES) void k_pull1(DevGraph g, DevS
         q.r = GOSSIP ? (uint32_t)j : (uint32_t)q.v;
       }
     };
+    // loads only: the bit is tested by resolve() where it is used, so the wave does not wait
+    // for these loads here (their vmcnt wait would also cover every younger load in flight)
     auto activity = [&](PullStage& q) {
       if (q.b < 0) return;
       const int64_t j = q.beg + lane;
-      bool a = false;
       q.am = 0;
+      q.aword = 0;
       if (j < q.end) {
-        // issued with (not after) the activity bit: both depend only on the neighbour id
+        // issued with (not after) the activity word: both depend only on the neighbour id
         if (packed) q.am = AWp[q.v];
-        a = bit_test(Ap, q.v);
-        if (CHURN && a)
-          a = !churn_dropped((uint32_t)(p.round - 1), gidx(g, u0 + q.b), gidx(g, q.v),
-                             p.churn_thr, p.cseed_lo, p.cseed_hi);
+        q.aword = Ap[q.v >> 5];
       }
+    };
+    auto resolve = [&](PullStage& q) {
+      const int64_t j = q.beg + lane;
+      bool a = j < q.end && ((q.aword >> (q.v & 31)) & 1u);
+      if (CHURN && a)
+        a = !churn_dropped((uint32_t)(p.round - 1), gidx(g, u0 + q.b), gidx(g, q.v), p.churn_thr,
+                           p.cseed_lo, p.cseed_hi);
       q.act = a;
     };
     auto next_bit = [](uint32_t& t) -> int {
@@ -361,6 +371,7 @@ __global__ __launch_bounds__(256, P2PG_PULL_WAVES) void k_pull1(DevGraph g, DevS
       const uint64_t need = fm & ~s1.s;
       uint64_t acc = 0;
       if (__ballot(need != 0ull)) {
+        resolve(s1);
         uint64_t m = __ballot(s1.act);
         uint32_t srow = s1.r;
         uint64_t sam = s1.am;
@@ -635,6 +646,27 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
+// Development builds (-DP2PG_PROF): wave clock per fused-kernel segment, summed into st.prof.
+#ifdef P2PG_PROF
+#define PROF_DECL uint64_t pf_[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}; uint64_t pt_ = __builtin_amdgcn_s_memtime();
+#define PROF_MARK(i)                                  \
+  do {                                                \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
+    pf_[i] += t_ - pt_;                               \
+    pt_ = t_;                                         \
+  } while (0)
+#define PROF_FLUSH \
+  if (lane == 0) for (int i_ = 0; i_ < 9; ++i_) atomicAdd(&st.prof[i_], (unsigned long long)pf_[i_]);
+#define PROF_PARAMS , uint64_t* pf_, uint64_t& pt_
+#define PROF_PASS , pf_, pt_
+#else
+#define PROF_DECL
+#define PROF_MARK(i)
+#define PROF_FLUSH
+#define PROF_PARAMS
+#define PROF_PASS
+#endif
+
 // LDS of one scatter wave: a GCHUNK x 64-word mask table (two 32-bit halves per word, so
 // 32-bit LDS atomics) and the compacted list of active (word, bit) entries.
 struct ScatterLds {
@@ -659,12 +691,12 @@ struct ScatterLds {
 // (row atomics).  Every
 // per-source value is a scalar load or a lane of a prefetched register: a vector load here
 // would make the wave wait (vmcnt) for its own in-flight row stores / atomics.
-template <bool CHURN, int K, bool STORE_E>
+template <bool CHURN, int K, bool STORE_E, class CT>
 __device__ __forceinline__ void scatter_row(const DevGraph& g, const DevState& st,
                                             const RoundParams& p, ScatterLds& L, int lane,
                                             int64_t v, int64_t rb, int64_t deg, int chunk,
                                             int sl, uint64_t f, uint32_t nbr, int nbr0,
-                                            uint64_t* c) {
+                                            CT* c PROF_PARAMS) {
   const int W = st.W;
   const int cur = p.round & 1, nxt = cur ^ 1;
   uint64_t* __restrict__ nx = st.next[nxt];
@@ -735,6 +767,7 @@ __device__ __forceinline__ void scatter_row(const DevGraph& g, const DevState& s
         base += (uint32_t)__popcll(mk);
       }
       wave_lds_sync();
+      PROF_MARK(6);
       const uint32_t n = total - lb < (uint32_t)GLIST ? total - lb : (uint32_t)GLIST;
       if constexpr (K > 0) {
         // a source whose whole adjacency is this chunk needs no range check on its picks
@@ -758,6 +791,7 @@ __device__ __forceinline__ void scatter_row(const DevGraph& g, const DevState& s
         }
       }
       wave_lds_sync();
+      PROF_MARK(7);
     }
   }
   const bool use_tbl = anyf && !all;
@@ -782,7 +816,7 @@ __device__ __forceinline__ void scatter_row(const DevGraph& g, const DevState& s
       } else if (valid) {
         Eo[(int64_t)nj * W + w] = dropped ? 0ull : x;
       }
-      if (!dropped && lane == 0) c[ST_SCATTER] += (uint64_t)__popcll(bal);
+      if (!dropped && lane == 0) c[ST_SCATTER] += (CT)__popcll(bal);
     } else {
       if (!bal) continue;
       const int64_t u = (int64_t)nj;
@@ -792,15 +826,16 @@ __device__ __forceinline__ void scatter_row(const DevGraph& g, const DevState& s
       if (x) atomicOr((unsigned long long*)&nx[u * W + w], (unsigned long long)x);
       if (lane == 0) {
         atomicOr(&Tn[u >> 5], 1u << (u & 31));
-        c[ST_SCATTER] += (uint64_t)__popcll(bal);
+        c[ST_SCATTER] += (CT)__popcll(bal);
       }
     }
   }
+  PROF_MARK(8);
 }
 
 // The scatter launch: tasks [task0, nwords) are 32-peer bitmap words (sources with deg <=
 // GCHUNK), tasks [nwords, nwords + n_hub) are (wide source, chunk) items.  task0 = nwords
-// runs the wide sources only (after k_gossip_fused has scattered the narrow ones).
+// runs the items only (fused rounds: the items of the pull hubs, deg > HUB_T).
 template <bool CHURN, int K, bool STORE_E>
 __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st, RoundParams p,
                                                         const int64_t* __restrict__ hub_items,
@@ -817,6 +852,7 @@ __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st,
   const int64_t ntasks = nwords + n_hub;
   const int nslices = (W + 63) >> 6;
   uint64_t c[STAT_N] = {0, 0, 0, 0, 0, 0, 0, 0};
+  PROF_DECL  // development builds: segment clocks of this kernel are not reported
 
   // lane j's neighbour datum for the chunk starting at slot rb + nb
   auto load_nbr = [&](int64_t rb, int nn) -> uint32_t {
@@ -862,7 +898,7 @@ __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st,
           rv2 = load_nbr(rb2, (int)deg2);
         }
         scatter_row<CHURN, K, STORE_E>(g, st, p, L, lane, base + b1, rb1, deg1, 0, 0, f1, rv1, 0,
-                                       c);
+                                       c PROF_PASS);
         b1 = b2;
         rb1 = rb2;
         deg1 = deg2;
@@ -897,22 +933,34 @@ __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st,
       for (int sl = 0; sl < nslices; ++sl) {
         const int w = sl * 64 + lane;
         const uint64_t f = w < W ? Fc[v * W + w] : 0ull;
-        scatter_row<CHURN, K, STORE_E>(g, st, p, L, lane, v, rb, deg, chunk, sl, f, rv, 0, c);
+        scatter_row<CHURN, K, STORE_E>(g, st, p, L, lane, v, rb, deg, chunk, sl, f, rv, 0, c PROF_PASS);
       }
     }
   }
   flush_stats(st.stats, c, lane);
 }
 
+// Active neighbours whose E words the fused kernel keeps in flight across a target's picks.
+#ifndef P2PG_FG
+#define P2PG_FG 8
+#endif
+constexpr int FG = P2PG_FG;
+
+
+
 // Gossip dense round r >= 1 after a dense round r-1: the pull of round r (k_pull1<false,
 // true>: arrivals = packed E[(r-1)&1] rows of the active neighbours) and, for every peer with
 // a first receipt, its own round-r pushes (scatter_row<STORE_E> into E[r&1]) in the same
 // pass.  The new frontier row goes straight from registers into the picks (no HBM round trip,
-// no second pass over the peers), and the Philox work of one target overlaps the gathers of
-// the next two, which are already in flight.  Hubs (deg > HUB_T) are pulled by k_pull_hub_*
+// no second pass over the peers), and the Philox work of one target overlaps the first
+// gathers of the next target, which are already in flight.  Hubs (deg > HUB_T) are pulled by k_pull_hub_*
 // and pushed by a chunk-item scatter launch over the hubs only.
+#ifndef P2PG_FUSED_WAVES
+#define P2PG_FUSED_WAVES 1
+#endif
 template <bool CHURN, int K>
-__global__ __launch_bounds__(256) void k_gossip_fused(DevGraph g, DevState st, RoundParams p) {
+__global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph g, DevState st,
+                                                                        RoundParams p) {
   __shared__ ScatterLds lds[WPB];
   const int lane = threadIdx.x & 63;
   const int wib = wave_in_block();
@@ -926,7 +974,10 @@ __global__ __launch_bounds__(256) void k_gossip_fused(DevGraph g, DevState st, R
   const int64_t ntasks = (V + 31) >> 5;
   const bool valid = lane < W;
   const uint64_t fm = valid ? full_mask(lane, W, st.M) : 0ull;
-  uint64_t c[STAT_N] = {0, 0, 0, 0, 0, 0, 0, 0};
+  // per-lane counters are 32-bit and per task (<= 32 peers, none a hub: no overflow), folded
+  // into wave-uniform 64-bit totals after each task (fewer live VGPRs than 64-bit lanes)
+  uint64_t tot[STAT_N] = {0, 0, 0, 0, 0, 0, 0, 0};
+  PROF_DECL
 
   for (int64_t task = (int64_t)blockIdx.x * WPB + wib; task < ntasks;
        task += (int64_t)gridDim.x * WPB) {
@@ -960,16 +1011,16 @@ __global__ __launch_bounds__(256) void k_gossip_fused(DevGraph g, DevState st, R
         q.rv = g.rev[j];
       }
     };
+    // loads only; gather() tests the bit (see k_pull1)
     auto activity = [&](PullStage& q) {
       if (q.b < 0) return;
       const int64_t j = q.beg + lane;
       q.am = 0;
-      bool a = false;
+      q.aword = 0;
       if (j < q.end) {
         q.am = AWp[q.v];
-        a = bit_test(Ap, q.v);
+        q.aword = Ap[q.v >> 5];
       }
-      q.act = a;
     };
     auto next_bit = [](uint32_t& t) -> int {
       if (!t) return -1;
@@ -978,24 +1029,67 @@ __global__ __launch_bounds__(256) void k_gossip_fused(DevGraph g, DevState st, R
       return b;
     };
 
-    uint32_t rest = todo;
-    PullStage s1, s2, s3;
-    issue(s1, next_bit(rest));
-    issue(s2, next_bit(rest));
-    activity(s1);
+    // L4: the first FG active neighbours' words of q go out into X; mr = q's active slots
+    // (of its first 64) still to gather
+    uint64_t X[FG];
+    auto gather = [&](const PullStage& q, uint64_t& mr) {
+      const uint64_t need = fm & ~q.s;
+      const int64_t jq = q.beg + lane;
+      uint64_t m = __ballot(jq < q.end && ((q.aword >> (q.v & 31)) & 1u));
+      // all slot ids / word masks first, then all FG loads back to back: a readlane between
+      // two loads would make the wave wait for the first one (merged vmcnt state)
+      uint32_t sv[FG];
+      uint64_t am[FG];
+      bool ok[FG];
+#pragma unroll
+      for (int k = 0; k < FG; ++k) {
+        sv[k] = 0u;
+        am[k] = 0ull;
+        ok[k] = m != 0ull;
+        if (m) {
+          const int idx = __builtin_ctzll(m);
+          m &= m - 1ull;
+          sv[k] = (uint32_t)__builtin_amdgcn_readlane((int)q.r, idx);
+          am[k] = (uint64_t)readlane64((int64_t)q.am, idx);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < FG; ++k) X[k] = src_word(Src, sv[k], W, lane, true, am[k], ok[k] && need);
+      mr = m;
+    };
+
+    // Software pipeline, per target t: rows L2(t+2) -> activity L3(t+1) -> gathers(t) ->
+    // consume(t).  The first gathers of target t+1 are issued BEFORE target t's stores and
+    // picks, so their latency hides behind t's Philox / LDS work.  The four stages rotate by
+    // unrolling (step(A,B,C,D), step(B,C,D,A), ...), never by copying: a register copy of a
+    // load still in flight would make the wave wait for it (and, vmcnt being in order, for
+    // every younger load and store) at the end of each target.
+    uint32_t c[STAT_N] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t aw = 0, sat = sat0;
-    while (s1.b >= 0) {
-      issue(s3, next_bit(rest));
-      activity(s2);
-      const int64_t u = u0 + s1.b;
-      const uint64_t deg = (uint64_t)(s1.end - s1.beg);
-      const uint64_t need = fm & ~s1.s;
+    uint32_t rest = todo;
+    PullStage sA, sB, sC, sD;
+    issue(sA, next_bit(rest));
+    issue(sB, next_bit(rest));
+    activity(sA);
+    if (sA.b >= 0) gather(sA, sA.mr);
+    activity(sB);
+    issue(sC, next_bit(rest));
+    PROF_MARK(5);
+
+    // consume a (gathers in X), advance b (gathers), c (activity), d (rows), then a's picks
+    auto step = [&](PullStage& a, PullStage& b, PullStage& cc, PullStage& d) {
+      const int64_t u = u0 + a.b;
+      const uint64_t deg = (uint64_t)(a.end - a.beg);
+      const uint64_t need = fm & ~a.s;
       uint64_t acc = 0;
-      if (__ballot(need != 0ull)) {
-        uint64_t m = __ballot(s1.act);
-        uint32_t srow = s1.r;
-        uint64_t sam = s1.am;
-        int64_t cb = s1.beg;
+#pragma unroll
+      for (int k = 0; k < FG; ++k) acc |= X[k];
+      PROF_MARK(0);
+      {
+        uint64_t m = a.mr;  // the rest of the first 64 slots, then further 64-slot chunks
+        uint32_t srow = a.r;
+        uint64_t sam = a.am;
+        int64_t cb = a.beg;
         for (;;) {
           while (m) {
             uint32_t sv[8];
@@ -1022,62 +1116,100 @@ __global__ __launch_bounds__(256) void k_gossip_fused(DevGraph g, DevState st, R
             for (int k = 0; k < 8; ++k) acc |= x[k];
           }
           cb += 64;
-          if (cb >= s1.end) break;
+          if (cb >= a.end) break;
           const int64_t j = cb + lane;  // further chunks of a wide row: serial
-          bool a = false;
+          bool act = false;
           srow = 0;
           sam = 0;
-          if (j < s1.end) {
+          if (j < a.end) {
             const int32_t v = g.colidx[j];
             srow = (uint32_t)j;
-            a = bit_test(Ap, v);
-            if (a) sam = AWp[v];
+            act = bit_test(Ap, v);
+            if (act) sam = AWp[v];
           }
-          m = __ballot(a);
+          m = __ballot(act);
         }
       }
+      // Everything loaded before this point (this target's rows, the next target's activity
+      // words) has landed or is about to: wait for it explicitly HERE, so that the compiler
+      // knows it has arrived and inserts no vmcnt wait behind the next target's gathers when
+      // this target's row words are used below (vmcnt is in order: such a wait would stall
+      // until those gathers return).
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+      PROF_MARK(1);
+      // advance the pipeline before this target's stores and picks: gathers of t+1 (their
+      // activity words were loaded a target ago), activity words of t+2, rows of t+3
+      if (b.b >= 0) gather(b, b.mr);
+      activity(cc);
+      issue(d, next_bit(rest));
+      PROF_MARK(2);
       const uint64_t nw = acc & need;
       const uint64_t wm = __ballot(nw != 0ull);
       if (nw) {
-        st.seen[u * W + lane] = s1.s | nw;
-        const uint64_t pc = (uint64_t)__popcll(nw);
-        const uint64_t per_bit = deg < (uint64_t)p.fanout ? deg : (uint64_t)p.fanout;
+        st.seen[u * W + lane] = a.s | nw;
+        const uint32_t pc = (uint32_t)__popcll(nw);
+        const uint32_t per_bit = deg < (uint64_t)p.fanout ? (uint32_t)deg : (uint32_t)p.fanout;
         c[ST_NEW] += pc;
         c[ST_RELAYS] += pc * per_bit;
         c[ST_ACTIVE_W] += 1;
-        c[ST_WEDGES] += deg;
+        c[ST_WEDGES] += (uint32_t)deg;
       }
       if (wm) {
         if (valid) Fc[u * W + lane] = nw;
-        aw |= 1u << s1.b;
+        aw |= 1u << a.b;
         if (lane == 0) {
           st.AW[cur][u] = wm;
           c[ST_ACTIVE_V] += 1;
-          c[ST_DEG_ACT] += deg;
+          c[ST_DEG_ACT] += (uint32_t)deg;
         }
-        // this round's pushes, GCHUNK connections at a time (s1.rv holds the receiver slots
-        // of the first 64; wider rows load the next 64 every 4 chunks)
-        uint32_t rvb = s1.rv;
-        for (int ch = 0; (int64_t)ch * GCHUNK < (int64_t)deg; ++ch) {
-          const int off = (ch * GCHUNK) & 63;
-          if (ch > 0 && off == 0) {
-            const int64_t j = s1.beg + (int64_t)ch * GCHUNK + lane;
-            rvb = j < s1.end ? g.rev[j] : 0u;
+        // this round's pushes, GCHUNK connections at a time.  a.rv holds the receiver slots of
+        // the first 64 (arrived: see the explicit wait above); wider rows load the next 64
+        // every 4 chunks and wait for them right there -- a load that MAY be in flight when
+        // the picks read the slots would make the compiler wait for everything, the next
+        // target's gathers included.
+        if (deg <= 64) {
+          for (int ch = 0; (int64_t)ch * GCHUNK < (int64_t)deg; ++ch)
+            scatter_row<CHURN, K, true>(g, st, p, lds[wib], lane, u, a.beg, (int64_t)deg, ch, 0,
+                                        nw, a.rv, ch * GCHUNK, c PROF_PASS);
+        } else {
+          for (int ch = 0; (int64_t)ch * GCHUNK < (int64_t)deg; ++ch) {
+            const int off = (ch * GCHUNK) & 63;
+            const int64_t j = a.beg + (int64_t)(ch * GCHUNK - off) + lane;
+            const uint32_t rvb = j < a.end ? g.rev[j] : 0u;
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+            scatter_row<CHURN, K, true>(g, st, p, lds[wib], lane, u, a.beg, (int64_t)deg, ch, 0,
+                                        nw, rvb, off, c PROF_PASS);
           }
-          scatter_row<CHURN, K, true>(g, st, p, lds[wib], lane, u, s1.beg, (int64_t)deg, ch, 0,
-                                      nw, rvb, off, c);
         }
       }
-      if (!__ballot(valid && (s1.s | nw) != fm)) sat |= 1u << s1.b;
-      s1 = s2;
-      s2 = s3;
+      PROF_MARK(3);
+      if (!__ballot(valid && (a.s | nw) != fm)) sat |= 1u << a.b;
+    };
+    for (;;) {
+      if (sA.b < 0) break;
+      step(sA, sB, sC, sD);
+      if (sB.b < 0) break;
+      step(sB, sC, sD, sA);
+      if (sC.b < 0) break;
+      step(sC, sD, sA, sB);
+      if (sD.b < 0) break;
+      step(sD, sA, sB, sC);
     }
+    PROF_MARK(4);
     if (lane == 0) {
       st.A[cur][task] = aw;
       if (sat != sat0) st.S[task] = sat;
     }
+#pragma unroll
+    for (int q = 0; q < STAT_N; ++q) tot[q] += wave_reduce_u32<false>(c[q]);
   }
-  flush_stats(st.stats, c, lane);
+  PROF_FLUSH
+  if (lane == 0) {
+    unsigned long long* shard = st.stats + (blockIdx.x & (STAT_SHARDS - 1)) * STAT_N;
+#pragma unroll
+    for (int q = 0; q < STAT_N; ++q)
+      if (tot[q]) atomicAdd(shard + q, (unsigned long long)tot[q]);
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1245,6 +1377,34 @@ __global__ void k_philox(int32_t n, const uint32_t* ctr, uint32_t k0, uint32_t k
   out[4 * i + 3] = r.w;
 }
 
+// Blocks of `kernel` (256 threads) that fit on the whole device at once: a persistent grid of
+// exactly this size has no second, partial wave of blocks (no tail).
+template <class F>
+int resident_blocks(F kernel) {
+  static const void* key[32];
+  static int val[32];
+  static int n = 0;
+  for (int i = 0; i < n; ++i)
+    if (key[i] == (const void*)kernel) return val[i];
+  int nb = 0, dev = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, 256, 0) != hipSuccess || nb < 1) nb = 1;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+    cus = 256;
+  const int r = nb * cus;
+  if (n < 32) {
+    key[n] = (const void*)kernel;
+    val[n] = r;
+    ++n;
+  }
+  return r;
+}
+
+int grid_tasks_uncapped(int64_t ntasks) {
+  const int64_t b = (ntasks + WPB - 1) / WPB;
+  return (int)(b < 1 ? 1 : (b > 0x7FFFFFFF ? 0x7FFFFFFF : b));
+}
+
 int grid_tasks(int64_t ntasks) {
   int64_t b = (ntasks + WPB - 1) / WPB;
   return (int)(b < 1 ? 1 : (b > GRID_MAX ? GRID_MAX : b));
@@ -1342,8 +1502,18 @@ hipError_t launch_gossip_fused(const DevGraph& g, const DevState& st, const Roun
   if (hp.n_items)
     hipLaunchKernelGGL((k_pull_hub_partial<false, true>), dim3(grid_tasks(hp.n_items)),
                        dim3(256), 0, s, g, st, p, hp);
-#define P2PG_FUSED(CH, KK) \
-  hipLaunchKernelGGL((k_gossip_fused<CH, KK>), dim3(grid), dim3(256), 0, s, g, st, p)
+  // grid = P2PG_FUSED_GRID x the blocks resident at once (default 2: blocks that finish early
+  // are replaced by the second set, which evens out the per-wave task cost)
+  static const int gmul = [] {
+    const char* e = std::getenv("P2PG_FUSED_GRID");
+    const int v = e ? std::atoi(e) : 2;
+    return v > 0 ? v : 2;
+  }();
+#define P2PG_FUSED(CH, KK)                                                                     \
+  hipLaunchKernelGGL((k_gossip_fused<CH, KK>),                                               \
+                     dim3(std::min<int64_t>((int64_t)grid_tasks_uncapped((g.V + 31) >> 5),    \
+                                            (int64_t)gmul * resident_blocks(k_gossip_fused<CH, KK>))), \
+                     dim3(256), 0, s, g, st, p)
   const bool ch = p.churn_thr != 0;
   switch (p.fanout) {
     case 1: if (ch) P2PG_FUSED(true, 1); else P2PG_FUSED(false, 1); break;

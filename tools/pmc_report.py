@@ -23,7 +23,7 @@ def load(d):
 
 
 def short(n):
-    for key in ("k_pull1", "k_pull", "k_gossip_update", "k_gossip_scatter", "k_record", "k_seed",
+    for key in ("k_gossip_fused", "k_pull1", "k_pull", "k_gossip_update", "k_gossip_scatter", "k_record", "k_seed",
                 "k_zero_rows", "fillBuffer", "copyBuffer"):
         if key in n:
             if key == "k_gossip_scatter":
