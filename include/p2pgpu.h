@@ -149,6 +149,27 @@ int p2pg_set_exchange(p2pg_engine* e, int64_t n_send, const int32_t* send_local,
                       const int32_t* recv_local);
 int p2pg_exchange_pack(p2pg_engine* e, int32_t plane, void* dev_buf);
 int p2pg_exchange_unpack(p2pg_engine* e, int32_t plane, const void* dev_buf);
+/* ---- dynamic topology --------------------------------------------
+ * Connection changes between rounds: n_add pairs to connect (Node.connect_with_node,
+ * node.py:122-176) and n_del pairs to disconnect (Node.disconnect_with_node, node.py:178-189,
+ * then node_disconnected on both ends, node.py:307-319), as 2*n peer ids (a0, b0, a1, b1..).
+ * Connecting an existing pair, disconnecting a missing one, self connections and pairs listed
+ * twice are errors (P2PG_ERR_ARG; the reference refuses them with a debug print).  Messages
+ * sent in the last round and still in flight on a removed connection are lost (a stopped
+ * NodeConnection drops its unread buffer, nodeconnection.py:192-228); the others arrive next
+ * round; every send from the next round on uses the new connections.  One update per round
+ * boundary; not on a vertex-partitioned rank.                                              */
+int p2pg_update_edges(p2pg_engine* e, int64_t n_add, const int32_t* add, int64_t n_del,
+                      const int32_t* del);
+/* ---- snapshot / resume (the reference has no checkpointing) --------
+ * Between rounds, the run state (round, seen sets, saturation, the last round's first
+ * receipts, messages in flight, hop/parent planes in record mode) is written to a caller
+ * buffer of p2pg_snapshot_size bytes, and read back by p2pg_restore into an engine with the
+ * same configuration, graph and sources (checked: P2PG_ERR_STATE otherwise), which then
+ * continues bit-identically.  Not between a topology update and the next round.           */
+int p2pg_snapshot_size(p2pg_engine* e, int64_t* bytes);
+int p2pg_snapshot(p2pg_engine* e, void* buf, int64_t cap);
+int p2pg_restore(p2pg_engine* e, const void* buf, int64_t size);
 /* Launch on this hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); NULL =
  * the engine's own stream.                                                              */
 int p2pg_set_stream(p2pg_engine* e, void* hip_stream);

@@ -74,8 +74,44 @@ def _check_csr(rowptr, colidx):
     return rowptr, colidx, V
 
 
-def flood(rowptr, colidx, src, churn_threshold=0, churn_seed=0, max_rounds=1 << 20):
-    """Flood relay with message-id dedup (forward to all connections except the sender)."""
+def _slots(rowptr, colidx, pairs):
+    """Slots of both directions of the undirected pairs (each must exist)."""
+    out = []
+    for a, b in np.asarray(pairs, dtype=np.int64).reshape(-1, 2):
+        for x, y in ((a, b), (b, a)):
+            row = colidx[rowptr[x]:rowptr[x + 1]]
+            k = int(np.searchsorted(row, y))
+            assert k < len(row) and row[k] == y, "removed connection does not exist"
+            out.append(rowptr[x] + k)
+    return np.asarray(out, dtype=np.int64)
+
+
+def _apply_changes(rowptr, colidx, add, remove):
+    """Topology after connecting `add` and disconnecting `remove` (undirected pairs), CSR
+    rows ascending -- Node.connect_with_node / disconnect_with_node between rounds."""
+    V = len(rowptr) - 1
+    rows = np.repeat(np.arange(V, dtype=np.int64), np.diff(rowptr))
+    keep = np.ones(len(colidx), dtype=bool)
+    keep[_slots(rowptr, colidx, remove)] = False
+    a = np.asarray(add, dtype=np.int64).reshape(-1, 2)
+    src = np.concatenate([rows[keep], a[:, 0], a[:, 1]])
+    dst = np.concatenate([colidx[keep], a[:, 1], a[:, 0]])
+    order = np.lexsort((dst, src))
+    src, dst = src[order], dst[order]
+    nrp = np.zeros(V + 1, dtype=np.int64)
+    np.cumsum(np.bincount(src, minlength=V), out=nrp[1:])
+    return nrp, dst.astype(np.int64)
+
+
+def flood(rowptr, colidx, src, churn_threshold=0, churn_seed=0, max_rounds=1 << 20,
+          updates=None):
+    """Flood relay with message-id dedup (forward to all connections except the sender).
+
+    updates: {r: (add_pairs, remove_pairs)} -- connection changes after round r.  The sends of
+    round r travel on the connections they were made on; those on removed connections are
+    lost in flight; the sends of round r+1 on use the new connections (include/p2pgpu.h
+    p2pg_update_edges)."""
+    updates = updates or {}
     rowptr, colidx, V = _check_csr(rowptr, colidx)
     src = np.asarray(src, dtype=np.int64)
     M = len(src)
@@ -98,6 +134,9 @@ def flood(rowptr, colidx, src, churn_threshold=0, churn_seed=0, max_rounds=1 << 
     while F.any() and rnd < max_rounds:
         rnd += 1
         alive = ~philox.churn_dropped(rnd - 1, rows, colidx, churn_threshold, churn_seed)
+        upd = updates.get(rnd - 1)
+        if upd is not None:
+            alive[_slots(rowptr, colidx, upd[1])] = False
         pending = np.zeros((V, M), dtype=bool)
         contrib = F[colidx] & alive[:, None]  # [E, M]: sender colidx[e] -> receiver rows[e]
         arr = np.zeros((V, M), dtype=bool)
@@ -117,6 +156,11 @@ def flood(rowptr, colidx, src, churn_threshold=0, churn_seed=0, max_rounds=1 << 
                 parent[us[r_i], m_i] = colidx[e[r_i]]
                 pending[us] &= ~hit
         assert not pending.any()
+        if upd is not None:  # the receipts of this round relay on the new connections
+            rowptr, colidx = _apply_changes(rowptr, colidx, upd[0], upd[1])
+            deg = np.diff(rowptr)
+            rows = np.repeat(np.arange(V), deg)
+            maxdeg = int(deg.max()) if V else 0
         seen |= new
         hop[new] = rnd
         F = new
@@ -125,9 +169,11 @@ def flood(rowptr, colidx, src, churn_threshold=0, churn_seed=0, max_rounds=1 << 
 
 
 def gossip(rowptr, colidx, src, fanout, gossip_seed, msg_id_base=0, churn_threshold=0,
-           churn_seed=0, max_rounds=1 << 20):
+           churn_seed=0, max_rounds=1 << 20, updates=None):
     """Push-gossip: on first receipt (or origination) in round r, peer v pushes m to
-    min(k, deg v) distinct neighbours picked by Philox(round, v, msg) (sender not excluded)."""
+    min(k, deg v) distinct neighbours picked by Philox(round, v, msg) (sender not excluded).
+    updates: as for flood()."""
+    updates = updates or {}
     rowptr, colidx, V = _check_csr(rowptr, colidx)
     src = np.asarray(src, dtype=np.int64)
     M = len(src)
@@ -178,6 +224,16 @@ def gossip(rowptr, colidx, src, fanout, gossip_seed, msg_id_base=0, churn_thresh
         res.rounds.append(pending_stats)
         if not len(vs) or rnd >= max_rounds:
             break
+        upd = updates.get(rnd)
+        if upd is not None:  # pushes on removed connections are lost; new picks, new lists
+            r = np.asarray(upd[1], dtype=np.int64).reshape(-1, 2)
+            gone = set(map(tuple, r.tolist())) | set(map(tuple, r[:, ::-1].tolist()))
+            if len(tgt) and gone:
+                keep = np.array([(int(a), int(b)) not in gone for a, b in zip(snd, tgt)], dtype=bool)
+                tgt, snd, msg = tgt[keep], snd[keep], msg[keep]
+            rowptr, colidx = _apply_changes(rowptr, colidx, upd[0], upd[1])
+            deg = np.diff(rowptr)
+            fan = np.minimum(deg, k)
         rnd += 1
         arr = np.zeros((V, M), dtype=bool)
         arr[tgt, msg] = True

@@ -35,6 +35,7 @@ struct p2pg_engine {
   int64_t V = 0, nnz = 0;
   int32_t M = 0, W = 0;
   std::vector<int64_t> h_rowptr;
+  std::vector<int32_t> h_colidx;  // host copy of the adjacency (topology updates, snapshots)
   std::vector<int32_t> h_src;
   // device
   int64_t* d_rowptr = nullptr;
@@ -78,6 +79,14 @@ struct p2pg_engine {
   int32_t round = 0;
   bool done = false;
   bool have_state = false;
+  // after a topology update: the graph the in-flight messages were sent on and its removed
+  // slots, kept for the parents (record / deliveries) of the round that receives them
+  int64_t* d_rowptr_arr = nullptr;
+  int32_t* d_colidx_arr = nullptr;
+  uint8_t* d_gone = nullptr;
+  int32_t arr_round = -1;       // the round whose arrivals travelled on that graph
+  bool consume_next = false;    // the next round consumes materialized rows (update kernel)
+  uint64_t total_relays = 0;    // relays since the last reset (= sum of message_count_send)
 };
 
 namespace {
@@ -132,7 +141,32 @@ void free_state(p2pg_engine* e) {
   e->have_state = false;
 }
 
+void free_arr(p2pg_engine* e) {
+  dfree(e->d_rowptr_arr);
+  dfree(e->d_colidx_arr);
+  dfree(e->d_gone);
+  e->arr_round = -1;
+}
+
+// the topology arrays only (rows, reverse slots, hub lists / plans)
+void free_topology(p2pg_engine* e) {
+  dfree(e->d_rowptr);
+  dfree(e->d_colidx);
+  dfree(e->d_hub);
+  dfree(e->d_hub_big);
+  dfree(e->d_rev);
+  dfree(e->d_H);
+  dfree(e->d_hub_items);
+  dfree(e->d_hubs);
+  dfree(e->d_hub_begin);
+  dfree(e->d_partial);
+  e->hp = HubPlan{};
+  e->n_hub = 0;
+  e->n_hub_big = 0;
+}
+
 void free_graph(p2pg_engine* e) {
+  free_arr(e);
   dfree(e->d_rowptr);
   dfree(e->d_colidx);
   dfree(e->d_hub);
@@ -168,7 +202,15 @@ RoundParams params(const p2pg_engine* e) {
 }
 
 DevGraph graph(const p2pg_engine* e) {
-  return DevGraph{e->d_rowptr, e->d_colidx, e->d_rev, e->d_H, e->d_gid, e->V};
+  return DevGraph{e->d_rowptr, e->d_colidx, e->d_rev, e->d_H, e->d_gid, nullptr, e->V};
+}
+
+// The graph round r's arrivals travelled on: the pre-update graph (with its removed slots) for
+// the round right after a topology update, else the current one.
+DevGraph graph_for_arrivals(const p2pg_engine* e, int32_t r) {
+  if (r == e->arr_round && e->d_rowptr_arr)
+    return DevGraph{e->d_rowptr_arr, e->d_colidx_arr, nullptr, nullptr, e->d_gid, e->d_gone, e->V};
+  return graph(e);
 }
 
 // Timed launch: kernel class cls in [0, P2PG_KCLASS_N) (see include/p2pgpu.h).
@@ -206,6 +248,27 @@ int resolve_timings(p2pg_engine* e) {
   return P2PG_OK;
 }
 
+// Dense-round edge-mask planes E, sized by the current nnz: one, or two for fused rounds
+// (round r pulls E[(r-1)&1], pushes E[r&1]); only if they fit with headroom -- else gossip
+// pushes by row atomics only.  Replaces any previous planes (their contents are dropped).
+int alloc_edge_planes(p2pg_engine* e) {
+  DevState& s = e->st;
+  if (s.E[1] == s.E[0]) s.E[1] = nullptr;
+  dfree(s.E[0]);
+  dfree(s.E[1]);
+  if (e->cfg.mode != P2PG_MODE_GOSSIP || !e->d_rev || e->push_mode == 1) return P2PG_OK;
+  const size_t eb = (size_t)e->nnz * e->W * sizeof(uint64_t);
+  size_t free_b = 0, total_b = 0;
+  if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || eb + ((size_t)4 << 30) >= free_b)
+    return P2PG_OK;
+  HIPCHK(e, hipMalloc((void**)&s.E[0], eb ? eb : 8));
+  s.E[1] = s.E[0];
+  if (e->W <= 64 && e->fused && hipMemGetInfo(&free_b, &total_b) == hipSuccess &&
+      eb + ((size_t)4 << 30) < free_b)
+    HIPCHK(e, hipMalloc((void**)&s.E[1], eb ? eb : 8));
+  return P2PG_OK;
+}
+
 int alloc_state(p2pg_engine* e) {
   free_state(e);
   DevState& s = e->st;
@@ -237,22 +300,12 @@ int alloc_state(p2pg_engine* e) {
     }
   }
   if ((rc = A((void**)&s.S, e->bm_bytes))) return rc;
-  if (gossip && e->d_rev && e->push_mode != 1) {
-    // dense-round edge-mask buffer, only if it fits with headroom (else row atomics only)
-    const size_t eb = (size_t)e->nnz * e->W * sizeof(uint64_t);
-    size_t free_b = 0, total_b = 0;
-    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && eb + ((size_t)4 << 30) < free_b) {
-      if ((rc = A((void**)&s.E[0], eb ? eb : 8))) return rc;
-      s.E[1] = s.E[0];
-      if (e->W <= 64) {  // packed E rows (see DevState::AW)
-        for (int i = 0; i < 2; ++i)
-          if ((rc = A((void**)&s.AW[i], sizeof(uint64_t) * (size_t)e->V))) return rc;
-        // second E plane for fused dense rounds (round r pulls E[(r-1)&1], pushes E[r&1])
-        if (e->fused && hipMemGetInfo(&free_b, &total_b) == hipSuccess &&
-            eb + ((size_t)4 << 30) < free_b)
-          if ((rc = A((void**)&s.E[1], eb ? eb : 8))) return rc;
-      }
-    }
+  if (gossip && e->W <= 64)  // packed E rows (see DevState::AW)
+    for (int i = 0; i < 2; ++i)
+      if ((rc = A((void**)&s.AW[i], sizeof(uint64_t) * (size_t)e->V))) return rc;
+  if ((rc = alloc_edge_planes(e))) {
+    free_state(e);
+    return rc;
   }
   if (rec) {
     const size_t hb = (size_t)e->V * e->M * sizeof(int32_t);
@@ -309,8 +362,14 @@ int p2pg_set_stream(p2pg_engine* e, void* hip_stream) {
   return P2PG_OK;
 }
 
-int p2pg_load_csr(p2pg_engine* e, int64_t V, const int64_t* rowptr, const int32_t* colidx) {
-  if (!e || V <= 0 || V > 0x7FFFFFFFll || !rowptr) return fail(e, P2PG_ERR_ARG, "load_csr: bad arguments");
+}  // extern "C"
+
+namespace {
+
+// Checks the CSR invariants the kernels rely on and builds the gossip reverse slots.
+int check_csr(p2pg_engine* e, int64_t V, const int64_t* rowptr, const int32_t* colidx,
+              std::vector<uint32_t>& rev) {
+  if (V <= 0 || V > 0x7FFFFFFFll || !rowptr) return fail(e, P2PG_ERR_ARG, "load_csr: bad arguments");
   const int64_t nnz = rowptr[V];
   if (rowptr[0] != 0 || nnz < 0 || (nnz > 0 && !colidx))
     return fail(e, P2PG_ERR_GRAPH, "load_csr: rowptr[0] must be 0 and rowptr[V] >= 0");
@@ -328,7 +387,7 @@ int p2pg_load_csr(p2pg_engine* e, int64_t V, const int64_t* rowptr, const int32_
   }
   // symmetry (every connection relays both ways, node.py:75-78) and reverse slots
   const bool local = (e->cfg.flags & P2PG_FLAG_LOCAL_GRAPH) != 0;
-  std::vector<uint32_t> rev(e->cfg.mode == P2PG_MODE_GOSSIP && !local && nnz < 0xFFFFFFFFll ? nnz : 0);
+  rev.assign(e->cfg.mode == P2PG_MODE_GOSSIP && !local && nnz < 0xFFFFFFFFll ? nnz : 0, 0u);
   int64_t asym = -1;
 #pragma omp parallel for schedule(dynamic, 4096)
   for (int64_t u = 0; u < V; ++u) {
@@ -347,9 +406,15 @@ int p2pg_load_csr(p2pg_engine* e, int64_t V, const int64_t* rowptr, const int32_
     }
   }
   if (asym >= 0) return fail(e, P2PG_ERR_GRAPH, "load_csr: adjacency not symmetric");
-  HIPCHK(e, hipSetDevice(e->cfg.device));
-  free_graph(e);
-  free_state(e);
+  return P2PG_OK;
+}
+
+// Device copies of a checked CSR (rows, reverse slots, gossip chunk items, pull hub plan);
+// replaces the engine's topology arrays, leaves the run state alone.
+int upload_graph(p2pg_engine* e, int64_t V, const int64_t* rowptr, const int32_t* colidx,
+                 const std::vector<uint32_t>& rev) {
+  const int64_t nnz = rowptr[V];
+  free_topology(e);
   e->V = V;
   e->nnz = nnz;
   if (!rev.empty()) {
@@ -357,6 +422,7 @@ int p2pg_load_csr(p2pg_engine* e, int64_t V, const int64_t* rowptr, const int32_
     HIPCHK(e, hipMemcpy(e->d_rev, rev.data(), sizeof(uint32_t) * rev.size(), hipMemcpyHostToDevice));
   }
   e->h_rowptr.assign(rowptr, rowptr + V + 1);
+  e->h_colidx.assign(colidx, colidx + nnz);
   HIPCHK(e, hipMalloc((void**)&e->d_rowptr, sizeof(int64_t) * (V + 1)));
   HIPCHK(e, hipMalloc((void**)&e->d_colidx, sizeof(int32_t) * (nnz ? nnz : 1)));
   HIPCHK(e, hipMemcpy(e->d_rowptr, rowptr, sizeof(int64_t) * (V + 1), hipMemcpyHostToDevice));
@@ -405,6 +471,22 @@ int p2pg_load_csr(p2pg_engine* e, int64_t V, const int64_t* rowptr, const int32_
   HIPCHK(e, hipMalloc((void**)&e->d_hub_big, sizeof(int64_t) * (hub_big.empty() ? 1 : hub_big.size())));
   if (!hub_big.empty())
     HIPCHK(e, hipMemcpy(e->d_hub_big, hub_big.data(), sizeof(int64_t) * hub_big.size(), hipMemcpyHostToDevice));
+  return P2PG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int p2pg_load_csr(p2pg_engine* e, int64_t V, const int64_t* rowptr, const int32_t* colidx) {
+  if (!e) return fail(e, P2PG_ERR_ARG, "load_csr: bad arguments");
+  std::vector<uint32_t> rev;
+  int rc = check_csr(e, V, rowptr, colidx, rev);
+  if (rc) return rc;
+  HIPCHK(e, hipSetDevice(e->cfg.device));
+  free_graph(e);
+  free_state(e);
+  if ((rc = upload_graph(e, V, rowptr, colidx, rev))) return rc;
   e->M = 0;
   e->W = 0;
   e->round = 0;
@@ -437,8 +519,8 @@ int p2pg_reset(p2pg_engine* e) {
   HIPCHK(e, hipMemsetAsync(s.seen, 0, e->plane_bytes, e->stream));
   HIPCHK(e, hipMemsetAsync(s.S, 0, e->bm_bytes, e->stream));
   for (int i = 0; i < 2; ++i) HIPCHK(e, hipMemsetAsync(s.A[i], 0, e->bm_bytes, e->stream));
-  if (e->cfg.mode == P2PG_MODE_GOSSIP && !e->done && e->round > 0) {
-    // an interrupted gossip run may leave pushes in flight: clear them
+  if (s.next[0] && ((!e->done && e->round > 0) || e->consume_next)) {
+    // an interrupted run may leave pushes / materialized arrivals in flight: clear them
     for (int i = 0; i < 2; ++i) {
       HIPCHK(e, hipMemsetAsync(s.next[i], 0, e->plane_bytes, e->stream));
       HIPCHK(e, hipMemsetAsync(s.T[i], 0, e->bm_bytes, e->stream));
@@ -451,6 +533,9 @@ int p2pg_reset(p2pg_engine* e) {
   e->round = 0;
   e->done = false;
   e->last_push_e = false;
+  e->consume_next = false;
+  e->total_relays = 0;
+  free_arr(e);
   e->prev_aw = e->prev_av = 0;
   for (int i = 0; i < P2PG_KCLASS_N; ++i) {
     e->kms[i] = 0;
@@ -470,6 +555,7 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
   }
   HIPCHK(e, hipSetDevice(e->cfg.device));
   DevState& s = e->st;
+  if (e->arr_round >= 0 && e->round > e->arr_round) free_arr(e);
   const DevGraph g = graph(e);
   const RoundParams p = params(e);
   const bool gossip = e->cfg.mode == P2PG_MODE_GOSSIP;
@@ -503,6 +589,10 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
       const int64_t v = x / e->W;
       host_wedge += (uint64_t)(e->h_rowptr[v + 1] - e->h_rowptr[v]);
     }
+  } else if (e->consume_next) {
+    // arrivals materialized into row pushes (topology update / restored snapshot)
+    if ((rc = timed(e, 4, [&] { return launch_gossip_update(g, s, p, e->stream); }))) return rc;
+    e->consume_next = false;
   } else if (!gossip) {
     if ((rc = timed(e, 1, [&] { return launch_flood_pull(g, s, p, e->hp, e->stream); }))) return rc;
   } else if (e->last_push_e) {
@@ -525,7 +615,10 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
     if ((rc = timed(e, 4, [&] { return launch_gossip_update(g, s, p, e->stream); }))) return rc;
   }
   if (s.hop)
-    if ((rc = timed(e, 3, [&] { return launch_record(g, s, p, e->stream); }))) return rc;
+    if ((rc = timed(e, 3, [&] {
+           return launch_record(graph_for_arrivals(e, e->round), s, p, e->stream);
+         })))
+      return rc;
   uint64_t tot[STAT_N] = {0};
   auto read_stats = [&]() -> int {
     HIPCHK(e, hipMemcpyAsync(e->h_stats, s.stats, sizeof(unsigned long long) * STAT_N * STAT_SHARDS,
@@ -584,6 +677,7 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
                      : fused_round ? P2PG_PUSH_FUSED
                      : e->last_push_e ? P2PG_PUSH_EDGE : P2PG_PUSH_ATOMIC;
   }
+  e->total_relays += tot[ST_RELAYS];
   e->prev_aw = tot[ST_ACTIVE_W];
   e->prev_av = tot[ST_ACTIVE_V];
   e->round += 1;
@@ -617,7 +711,7 @@ int p2pg_get_new_deliveries(p2pg_engine* e, int64_t cap, int32_t* peer, int32_t*
   // the most recent round is e->round - 1; its frontier is F[(round-1)&1]
   RoundParams p = params(e);
   p.round = e->round - 1;
-  const DevGraph g = graph(e);
+  const DevGraph g = graph_for_arrivals(e, p.round);
   int32_t *dpeer = nullptr, *dmsg = nullptr, *dpar = nullptr;
   unsigned long long* dcnt = nullptr;
   const int64_t c = cap > 0 ? cap : 1;
@@ -738,6 +832,307 @@ int p2pg_exchange_pack(p2pg_engine* e, int32_t plane, void* dev_buf) {
 
 int p2pg_exchange_unpack(p2pg_engine* e, int32_t plane, const void* dev_buf) {
   return exchange(e, plane, false, const_cast<void*>(dev_buf));
+}
+
+int p2pg_update_edges(p2pg_engine* e, int64_t n_add, const int32_t* add, int64_t n_del,
+                      const int32_t* del) {
+  if (!e || !e->d_rowptr || n_add < 0 || n_del < 0 || (n_add && !add) || (n_del && !del))
+    return fail(e, P2PG_ERR_ARG, "update_edges: bad arguments");
+  if (e->d_gid || (e->cfg.flags & P2PG_FLAG_LOCAL_GRAPH))
+    return fail(e, P2PG_ERR_STATE, "update_edges: not supported on a vertex-partitioned rank");
+  if (e->arr_round >= 0 && e->arr_round == e->round)
+    return fail(e, P2PG_ERR_STATE, "update_edges: one update per round boundary");
+  const int64_t V = e->V;
+  const std::vector<int64_t>& rp = e->h_rowptr;
+  const std::vector<int32_t>& ci = e->h_colidx;
+  auto slot_of = [&](int32_t a, int32_t b) -> int64_t {  // slot of b in a's row, or -1
+    const int32_t* beg = ci.data() + rp[a];
+    const int32_t* end = ci.data() + rp[a + 1];
+    const int32_t* it = std::lower_bound(beg, end, b);
+    return (it != end && *it == b) ? (int64_t)(it - ci.data()) : -1;
+  };
+  // both directions of every change, sorted by (row, neighbour)
+  std::vector<std::pair<int32_t, int32_t>> adds, dels;
+  auto collect = [&](int64_t n, const int32_t* pr, bool is_add,
+                     std::vector<std::pair<int32_t, int32_t>>& out) -> int {
+    for (int64_t i = 0; i < n; ++i) {
+      const int32_t a = pr[2 * i], b = pr[2 * i + 1];
+      if (a < 0 || b < 0 || a >= V || b >= V)
+        return fail(e, P2PG_ERR_ARG, "update_edges: peer id out of range");
+      if (a == b)  // node.py:131-133 refuses self connections
+        return fail(e, P2PG_ERR_ARG, "update_edges: self connection");
+      const bool exists = slot_of(a, b) >= 0;
+      if (is_add && exists)  // node.py:136-139: already connected
+        return fail(e, P2PG_ERR_ARG, "update_edges: connection already exists");
+      if (!is_add && !exists)  // node.py:178-189: not connected
+        return fail(e, P2PG_ERR_ARG, "update_edges: no such connection");
+      out.emplace_back(a, b);
+      out.emplace_back(b, a);
+    }
+    std::sort(out.begin(), out.end());
+    if (std::adjacent_find(out.begin(), out.end()) != out.end())
+      return fail(e, P2PG_ERR_ARG, "update_edges: a connection is listed twice");
+    return P2PG_OK;
+  };
+  int rc;
+  if ((rc = collect(n_add, add, true, adds))) return rc;
+  if ((rc = collect(n_del, del, false, dels))) return rc;
+  HIPCHK(e, hipSetDevice(e->cfg.device));
+  // new adjacency: each row = old row - removed + added, ascending
+  std::vector<int64_t> nrp(V + 1, 0);
+  std::vector<int32_t> nci;
+  nci.reserve(ci.size() + adds.size());
+  {
+    size_t ia = 0, id = 0;
+    for (int64_t v = 0; v < V; ++v) {
+      std::vector<int32_t> plus;
+      while (ia < adds.size() && adds[ia].first == v) plus.push_back(adds[ia++].second);
+      size_t k = 0;
+      for (int64_t j = rp[v]; j < rp[v + 1]; ++j) {
+        const int32_t u = ci[j];
+        if (id < dels.size() && dels[id].first == v && dels[id].second == u) {
+          ++id;
+          continue;
+        }
+        while (k < plus.size() && plus[k] < u) nci.push_back(plus[k++]);
+        nci.push_back(u);
+      }
+      while (k < plus.size()) nci.push_back(plus[k++]);
+      nrp[v + 1] = (int64_t)nci.size();
+    }
+  }
+  const bool running = e->have_state && e->round > 0 && !e->done;
+  if (running) {
+    // Messages sent in the last round are in flight on the OLD connections: the ones on removed
+    // connections are lost (a stopped NodeConnection drops its unread buffer,
+    // nodeconnection.py:192-228), the rest arrive next round.  Materialize them as row pushes
+    // next[round&1] over the old graph minus the removed slots, before the graph changes.
+    DevState& s = e->st;
+    const bool gossip = e->cfg.mode == P2PG_MODE_GOSSIP;
+    free_arr(e);
+    std::vector<uint8_t> gone(ci.size(), 0);
+    for (const auto& d : dels) gone[slot_of(d.first, d.second)] = 1;
+    HIPCHK(e, hipMalloc((void**)&e->d_gone, gone.empty() ? 1 : gone.size()));
+    if (!gone.empty()) HIPCHK(e, hipMemcpy(e->d_gone, gone.data(), gone.size(), hipMemcpyHostToDevice));
+    if (!s.next[0]) {  // flood: row-push planes on first use
+      for (int i = 0; i < 2; ++i) {
+        HIPCHK(e, hipMalloc((void**)&s.next[i], e->plane_bytes ? e->plane_bytes : 8));
+        HIPCHK(e, hipMalloc((void**)&s.T[i], e->bm_bytes ? e->bm_bytes : 8));
+        HIPCHK(e, hipMemsetAsync(s.next[i], 0, e->plane_bytes, e->stream));
+        HIPCHK(e, hipMemsetAsync(s.T[i], 0, e->bm_bytes, e->stream));
+      }
+    }
+    DevGraph gold = graph(e);
+    gold.gone = e->d_gone;
+    RoundParams p = params(e);
+    const int nx = e->round & 1;
+    hipError_t lr;
+    if (!gossip) {
+      if (!e->consume_next) {
+        lr = launch_materialize(gold, s, p, true, e->stream);
+        if (lr != hipSuccess) return fail(e, P2PG_ERR_HIP, std::string("update_edges: ") + hipGetErrorString(lr));
+      }
+    } else {
+      // the pushes of the last round, recomputed (Philox picks are a pure function of the
+      // round, peer and message) as row atomics over the old graph without the removed slots
+      HIPCHK(e, hipMemsetAsync(s.next[nx], 0, e->plane_bytes, e->stream));
+      HIPCHK(e, hipMemsetAsync(s.T[nx], 0, e->bm_bytes, e->stream));
+      p.round = e->round - 1;
+      lr = launch_gossip_scatter(gold, s, p, e->d_hub, e->n_hub, false, e->stream);
+      if (lr != hipSuccess) return fail(e, P2PG_ERR_HIP, std::string("update_edges: ") + hipGetErrorString(lr));
+    }
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    e->consume_next = true;
+    e->last_push_e = false;
+    // keep the old rows for the parents of the receiving round (record / deliveries)
+    e->d_rowptr_arr = e->d_rowptr;
+    e->d_colidx_arr = e->d_colidx;
+    e->d_rowptr = nullptr;
+    e->d_colidx = nullptr;
+    e->arr_round = e->round;
+  }
+  std::vector<uint32_t> rev;
+  if ((rc = check_csr(e, V, nrp.data(), nci.data(), rev))) return rc;
+  if ((rc = upload_graph(e, V, nrp.data(), nci.data(), rev))) return rc;
+  if (e->have_state && (rc = alloc_edge_planes(e))) return rc;
+  return P2PG_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+constexpr uint64_t SNAP_MAGIC = 0x50414E5347503250ull;  // "P2PGSNAP"
+constexpr uint32_t SNAP_VERSION = 1;
+
+struct SnapHeader {
+  uint64_t magic;
+  uint32_t version, mode;
+  int64_t V, nnz;
+  int32_t M, W, fanout, round;
+  uint32_t flags, churn_threshold, msg_id_base, done;
+  uint32_t consume_next, has_next;
+  uint64_t gossip_seed, churn_seed, graph_hash, src_hash, total_relays, prev_aw, prev_av;
+};
+
+uint64_t fnv1a(uint64_t h, const void* data, size_t n) {
+  const unsigned char* p = (const unsigned char*)data;
+  for (size_t i = 0; i < n; ++i) {
+    h ^= p[i];
+    h *= 0x100000001B3ull;
+  }
+  return h;
+}
+
+uint64_t graph_hash(const p2pg_engine* e) {
+  uint64_t h = fnv1a(0xCBF29CE484222325ull, e->h_rowptr.data(), e->h_rowptr.size() * sizeof(int64_t));
+  return fnv1a(h, e->h_colidx.data(), e->h_colidx.size() * sizeof(int32_t));
+}
+
+int64_t snapshot_bytes(const p2pg_engine* e) {
+  int64_t n = (int64_t)sizeof(SnapHeader) + 2 * (int64_t)e->plane_bytes + 2 * (int64_t)e->bm_bytes;
+  if (e->st.next[0]) n += (int64_t)e->plane_bytes + (int64_t)e->bm_bytes;
+  if (e->st.hop) n += 2 * (int64_t)e->V * e->M * (int64_t)sizeof(int32_t);
+  return n;
+}
+
+// The planes of a snapshot, in order: seen, saturated bits, the last round's activity bits and
+// frontier (its first receipts), [pending row pushes + their bits], [hop, parent].
+template <class F>
+int for_planes(p2pg_engine* e, F&& f) {
+  DevState& s = e->st;
+  const int last = (e->round + 1) & 1;  // (round - 1) & 1
+  const int nx = e->round & 1;
+  int rc;
+  if ((rc = f((void*)s.seen, e->plane_bytes))) return rc;
+  if ((rc = f((void*)s.S, e->bm_bytes))) return rc;
+  if ((rc = f((void*)s.A[last], e->bm_bytes))) return rc;
+  if ((rc = f((void*)s.F[last], e->plane_bytes))) return rc;
+  if (s.next[0]) {
+    if ((rc = f((void*)s.next[nx], e->plane_bytes))) return rc;
+    if ((rc = f((void*)s.T[nx], e->bm_bytes))) return rc;
+  }
+  if (s.hop) {
+    const size_t hb = (size_t)e->V * e->M * sizeof(int32_t);
+    if ((rc = f((void*)s.hop, hb))) return rc;
+    if ((rc = f((void*)s.parent, hb))) return rc;
+  }
+  return P2PG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int p2pg_snapshot_size(p2pg_engine* e, int64_t* bytes) {
+  if (!e || !bytes) return fail(e, P2PG_ERR_ARG, "snapshot_size: bad arguments");
+  if (!e->have_state) return fail(e, P2PG_ERR_STATE, "snapshot_size: no sources set");
+  *bytes = snapshot_bytes(e);
+  return P2PG_OK;
+}
+
+int p2pg_snapshot(p2pg_engine* e, void* buf, int64_t cap) {
+  if (!e || !buf) return fail(e, P2PG_ERR_ARG, "snapshot: bad arguments");
+  if (!e->have_state) return fail(e, P2PG_ERR_STATE, "snapshot: no sources set");
+  if (e->arr_round >= 0 && e->arr_round == e->round)
+    return fail(e, P2PG_ERR_STATE, "snapshot: take it before a topology update or after the next round");
+  HIPCHK(e, hipSetDevice(e->cfg.device));
+  DevState& s = e->st;
+  if (e->cfg.mode == P2PG_MODE_GOSSIP && e->last_push_e && e->round > 0 && !e->done) {
+    // pushes held per connection (E) -> row pushes, so the state does not depend on slots
+    RoundParams p = params(e);
+    hipError_t lr = launch_materialize(graph(e), s, p, false, e->stream);
+    if (lr != hipSuccess) return fail(e, P2PG_ERR_HIP, std::string("snapshot: ") + hipGetErrorString(lr));
+    e->last_push_e = false;
+  }
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  const int64_t need = snapshot_bytes(e);
+  if (cap < need) return fail(e, P2PG_ERR_ARG, "snapshot: buffer smaller than p2pg_snapshot_size");
+  SnapHeader h{};
+  h.magic = SNAP_MAGIC;
+  h.version = SNAP_VERSION;
+  h.mode = (uint32_t)e->cfg.mode;
+  h.V = e->V;
+  h.nnz = e->nnz;
+  h.M = e->M;
+  h.W = e->W;
+  h.fanout = e->cfg.fanout;
+  h.round = e->round;
+  h.flags = e->cfg.flags & P2PG_FLAG_RECORD;
+  h.churn_threshold = e->cfg.churn_threshold;
+  h.msg_id_base = e->cfg.msg_id_base;
+  h.done = e->done ? 1u : 0u;
+  h.consume_next = e->consume_next ? 1u : 0u;
+  h.has_next = s.next[0] ? 1u : 0u;
+  h.gossip_seed = e->cfg.gossip_seed;
+  h.churn_seed = e->cfg.churn_seed;
+  h.graph_hash = graph_hash(e);
+  h.src_hash = fnv1a(0xCBF29CE484222325ull, e->h_src.data(), e->h_src.size() * sizeof(int32_t));
+  h.total_relays = e->total_relays;
+  h.prev_aw = e->prev_aw;
+  h.prev_av = e->prev_av;
+  char* out = (char*)buf;
+  std::memcpy(out, &h, sizeof(h));
+  size_t off = sizeof(h);
+  return for_planes(e, [&](void* dev, size_t n) -> int {
+    if (n) HIPCHK(e, hipMemcpy(out + off, dev, n, hipMemcpyDeviceToHost));
+    off += n;
+    return P2PG_OK;
+  });
+}
+
+int p2pg_restore(p2pg_engine* e, const void* buf, int64_t size) {
+  if (!e || !buf || size < (int64_t)sizeof(SnapHeader)) return fail(e, P2PG_ERR_ARG, "restore: bad arguments");
+  if (!e->have_state) return fail(e, P2PG_ERR_STATE, "restore: set the same sources first");
+  SnapHeader h;
+  std::memcpy(&h, buf, sizeof(h));
+  if (h.magic != SNAP_MAGIC || h.version != SNAP_VERSION)
+    return fail(e, P2PG_ERR_ARG, "restore: not a relay-engine snapshot");
+  if (h.mode != (uint32_t)e->cfg.mode || h.fanout != e->cfg.fanout ||
+      h.gossip_seed != e->cfg.gossip_seed || h.churn_seed != e->cfg.churn_seed ||
+      h.churn_threshold != e->cfg.churn_threshold || h.msg_id_base != e->cfg.msg_id_base ||
+      h.flags != (e->cfg.flags & P2PG_FLAG_RECORD))
+    return fail(e, P2PG_ERR_STATE, "restore: engine configuration differs from the snapshot's");
+  if (h.V != e->V || h.nnz != e->nnz || h.graph_hash != graph_hash(e))
+    return fail(e, P2PG_ERR_STATE, "restore: graph differs from the snapshot's");
+  if (h.M != e->M || h.src_hash != fnv1a(0xCBF29CE484222325ull, e->h_src.data(), e->h_src.size() * sizeof(int32_t)))
+    return fail(e, P2PG_ERR_STATE, "restore: broadcast sources differ from the snapshot's");
+  HIPCHK(e, hipSetDevice(e->cfg.device));
+  int rc = p2pg_reset(e);
+  if (rc) return rc;
+  DevState& s = e->st;
+  if (h.has_next && !s.next[0]) {  // flood run that had a topology update
+    for (int i = 0; i < 2; ++i) {
+      HIPCHK(e, hipMalloc((void**)&s.next[i], e->plane_bytes ? e->plane_bytes : 8));
+      HIPCHK(e, hipMalloc((void**)&s.T[i], e->bm_bytes ? e->bm_bytes : 8));
+    }
+  }
+  if (s.next[0]) {
+    for (int i = 0; i < 2; ++i) {
+      HIPCHK(e, hipMemsetAsync(s.next[i], 0, e->plane_bytes, e->stream));
+      HIPCHK(e, hipMemsetAsync(s.T[i], 0, e->bm_bytes, e->stream));
+    }
+  }
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  e->round = h.round;
+  e->done = h.done != 0;
+  e->consume_next = h.consume_next != 0;
+  e->last_push_e = false;
+  e->total_relays = h.total_relays;
+  e->prev_aw = h.prev_aw;
+  e->prev_av = h.prev_av;
+  if (size < snapshot_bytes(e) || (h.has_next != 0) != (s.next[0] != nullptr))
+    return fail(e, P2PG_ERR_ARG, "restore: snapshot truncated or of another layout");
+  const char* in = (const char*)buf;
+  size_t off = sizeof(h);
+  rc = for_planes(e, [&](void* dev, size_t n) -> int {
+    if (n) HIPCHK(e, hipMemcpy(dev, in + off, n, hipMemcpyHostToDevice));
+    off += n;
+    return P2PG_OK;
+  });
+  if (rc) return rc;
+  HIPCHK(e, hipMemsetAsync(s.A[e->round & 1], 0, e->bm_bytes, e->stream));
+  return P2PG_OK;
 }
 
 int p2pg_kernel_times(p2pg_engine* e, double ms[P2PG_KCLASS_N], int64_t launches[P2PG_KCLASS_N]) {

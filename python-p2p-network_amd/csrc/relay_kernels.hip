@@ -598,7 +598,10 @@ __global__ __launch_bounds__(256) void k_gossip_update(DevGraph g, DevState st,
       tw &= tw - 1u;
       const int64_t u = (task << 5) + b;
       const int64_t deg = g.rowptr[u + 1] - g.rowptr[u];
-      const uint64_t fan = (uint64_t)(deg < p.fanout ? deg : p.fanout);
+      // relays per first receipt: gossip min(k, deg); flood (rows materialized by a topology
+      // update) deg - 1, the sender's connection being excluded (node.py:106-112)
+      const uint64_t fan = p.mode == 0 ? (uint64_t)(deg > 0 ? deg - 1 : 0)
+                                       : (uint64_t)(deg < p.fanout ? deg : p.fanout);
       bool row_new = false;
       for (int sl = 0; sl < nslices; ++sl) {
         const int w = sl * 64 + lane;
@@ -638,6 +641,52 @@ __global__ __launch_bounds__(256) void k_gossip_update(DevGraph g, DevState st,
     if (lane == 0) st.A[cur][task] = aw;
   }
   flush_stats(st.stats, c, lane);
+}
+
+// Messages in flight after round r = p.round - 1, as row pushes into next[p.round&1] + T bits
+// (the form k_gossip_update consumes), one wave per receiver u, lane = word, serial over u's
+// slots (not a hot path):
+//   FLOOD = false: gossip pushes held per connection in E[r&1] (a dense round), so that the
+//                  run state no longer depends on slot numbering (snapshots);
+//   FLOOD = true:  flood sends of round r = the frontier rows F[r&1] of u's active neighbours
+//                  (churn of round r applied), over g -- the graph they were sent on -- minus
+//                  the slots a topology update removed (g.gone).
+template <bool FLOOD>
+__global__ __launch_bounds__(256) void k_materialize(DevGraph g, DevState st, RoundParams p) {
+  const int lane = threadIdx.x & 63;
+  const int W = st.W;
+  const int cur = p.round & 1, prv = cur ^ 1;
+  const uint64_t* __restrict__ Src = FLOOD ? st.F[prv] : st.E[prv];
+  const uint32_t* __restrict__ Ap = st.A[prv];
+  const uint64_t* __restrict__ AWp = FLOOD ? nullptr : st.AW[prv];
+  const bool packed = AWp != nullptr;
+  const int nslices = (W + 63) >> 6;
+  for (int64_t u = (int64_t)blockIdx.x * WPB + wave_in_block(); u < g.V;
+       u += (int64_t)gridDim.x * WPB) {
+    const int64_t beg = g.rowptr[u], end = g.rowptr[u + 1];
+    bool any = false;
+    for (int sl = 0; sl < nslices; ++sl) {
+      const int w = sl * 64 + lane;
+      uint64_t acc = 0;
+      for (int64_t j = beg; j < end; ++j) {
+        const int32_t v = g.colidx[j];
+        if (!bit_test(Ap, v)) continue;
+        if (FLOOD) {
+          if (g.gone && g.gone[j]) continue;
+          if (p.churn_thr && churn_dropped((uint32_t)(p.round - 1), gidx(g, u), gidx(g, v),
+                                           p.churn_thr, p.cseed_lo, p.cseed_hi))
+            continue;
+          acc |= w < W ? Src[(int64_t)v * W + w] : 0ull;
+        } else {
+          acc |= packed ? src_word(Src, (uint32_t)j, W, lane, true, AWp[v], true)
+                        : (w < W ? Src[j * W + w] : 0ull);
+        }
+      }
+      if (acc) st.next[cur][u * W + w] |= acc;
+      any |= __ballot(acc != 0ull) != 0ull;
+    }
+    if (any && lane == 0) atomicOr(&st.T[cur][u >> 5], 1u << (u & 31));
+  }
 }
 
 // Orders this wave's LDS writes before its later LDS reads by other lanes.
@@ -819,6 +868,7 @@ __device__ __forceinline__ void scatter_row(const DevGraph& g, const DevState& s
       if (!dropped && lane == 0) c[ST_SCATTER] += (CT)__popcll(bal);
     } else {
       if (!bal) continue;
+      if (g.gone && g.gone[rb + nb + j]) continue;  // connection removed: the push is lost
       const int64_t u = (int64_t)nj;
       if (CHURN && churn_dropped((uint32_t)p.round, gv, gidx_s(g, u), p.churn_thr,
                                  p.cseed_lo, p.cseed_hi))
@@ -1225,6 +1275,7 @@ __device__ int32_t find_parent(const DevGraph& g, const DevState& st, const Roun
   const int64_t beg = g.rowptr[u], end = g.rowptr[u + 1];
   for (int64_t e = beg; e < end; ++e) {
     const int32_t v = g.colidx[e];
+    if (g.gone && g.gone[e]) continue;  // lost with its connection (topology update)
     if (!bit_test(st.A[prv], v)) continue;
     if (!(st.F[prv][(int64_t)v * W + w] & bit)) continue;
     if (p.churn_thr && churn_dropped((uint32_t)(p.round - 1), gidx(g, u), gidx(g, v),
@@ -1456,6 +1507,16 @@ hipError_t launch_flood_pull(const DevGraph& g, const DevState& st, const RoundP
 hipError_t launch_gossip_pull(const DevGraph& g, const DevState& st, const RoundParams& p,
                               const HubPlan& hp, hipStream_t s) {
   return pull_with_hubs<false, true>(g, st, p, hp, s);
+}
+
+hipError_t launch_materialize(const DevGraph& g, const DevState& st, const RoundParams& p,
+                              bool flood, hipStream_t s) {
+  const int grid = grid_tasks(g.V);
+  if (flood)
+    hipLaunchKernelGGL(k_materialize<true>, dim3(grid), dim3(256), 0, s, g, st, p);
+  else
+    hipLaunchKernelGGL(k_materialize<false>, dim3(grid), dim3(256), 0, s, g, st, p);
+  return hipGetLastError();
 }
 
 hipError_t launch_gossip_update(const DevGraph& g, const DevState& st, const RoundParams& p,

@@ -94,6 +94,10 @@ SIGNATURES = {
     "p2pg_exchange_unpack": (ctypes.c_int, [_P, _I32, _P]),
     "p2pg_set_stream": (ctypes.c_int, [_P, _P]),
     "p2pg_device_philox": (ctypes.c_int, [_P, _I32, _P, _P, _P]),
+    "p2pg_update_edges": (ctypes.c_int, [_P, _I64, _P, _I64, _P]),
+    "p2pg_snapshot_size": (ctypes.c_int, [_P, ctypes.POINTER(_I64)]),
+    "p2pg_snapshot": (ctypes.c_int, [_P, _P, _I64]),
+    "p2pg_restore": (ctypes.c_int, [_P, _P, _I64]),
     "p2pg_last_error": (ctypes.c_char_p, [_P]),
     "p2pg_global_error": (ctypes.c_char_p, []),
     "p2pg_destroy": (None, [_P]),

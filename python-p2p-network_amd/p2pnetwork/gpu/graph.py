@@ -59,6 +59,22 @@ class PeerGraph:
             raise ValueError("PeerGraph: adjacency must be symmetric")
         return self
 
+    def with_changes(self, add=(), remove=()):
+        """The topology after connecting the pairs in ``add`` and disconnecting those in
+        ``remove`` (undirected (a, b) pairs) -- what GraphNetwork.update_edges applies."""
+        V = self.V
+        rows = np.repeat(np.arange(V, dtype=np.int64), self.degree())
+        key = rows * V + self.colidx
+        a = np.asarray(add, dtype=np.int64).reshape(-1, 2)
+        r = np.asarray(remove, dtype=np.int64).reshape(-1, 2)
+        rk = np.concatenate([r[:, 0] * V + r[:, 1], r[:, 1] * V + r[:, 0]])
+        ak = np.concatenate([a[:, 0] * V + a[:, 1], a[:, 1] * V + a[:, 0]])
+        key = np.union1d(np.setdiff1d(key, rk), ak)
+        src, dst = key // V, key % V
+        rowptr = np.zeros(V + 1, dtype=np.int64)
+        np.cumsum(np.bincount(src, minlength=V), out=rowptr[1:])
+        return PeerGraph(rowptr, dst.astype(np.int32))
+
     # ---- construction through the library's host generators ---------------------------
     @classmethod
     def _from_handle(cls, h):

@@ -67,6 +67,12 @@ class Deliveries:
         return len(self.peer)
 
 
+# index of SnapHeader.total_relays in the snapshot header viewed as uint64 words (engine.cpp:
+# magic 0, version/mode 1, V 2, nnz 3, M/W 4, fanout/round 5, flags/thr 6, base/done 7,
+# consume/has_next 8, gossip_seed 9, churn_seed 10, graph_hash 11, src_hash 12, total_relays 13)
+_SNAP_TOTAL_RELAYS_WORD = 13
+
+
 def churn_threshold(p_drop):
     """floor(p_drop * 2^32), the integer threshold of the per-round edge-drop mask."""
     if not 0.0 <= p_drop < 1.0:
@@ -196,6 +202,48 @@ class GraphNetwork:
             if not st.active:
                 break
         return out
+
+    # -- topology changes between rounds ------------------------------
+    def update_edges(self, add=(), remove=()):
+        """Connect the (a, b) pairs in ``add`` (Node.connect_with_node, node.py:122-176) and
+        disconnect those in ``remove`` (Node.disconnect_with_node, node.py:178-189) between
+        rounds.  Messages in flight on a removed connection are lost; every send from the next
+        round on uses the new connections (include/p2pgpu.h p2pg_update_edges)."""
+        a = np.ascontiguousarray(np.asarray(add, dtype=np.int32).reshape(-1, 2))
+        r = np.ascontiguousarray(np.asarray(remove, dtype=np.int32).reshape(-1, 2))
+        self._check(_lib.lib().p2pg_update_edges(self._h, len(a), _lib.ptr(a) if len(a) else None,
+                                                 len(r), _lib.ptr(r) if len(r) else None))
+        self.graph = self.graph.with_changes(a, r)
+
+    def connect(self, pairs):
+        self.update_edges(add=pairs)
+
+    def disconnect(self, pairs):
+        self.update_edges(remove=pairs)
+
+    # -- snapshot / resume (SURVEY.md 8f rank 4) ------------------------------------------
+    def snapshot(self):
+        """The run state between rounds as a uint8 array (p2pg_snapshot)."""
+        n = ctypes.c_int64()
+        self._check(_lib.lib().p2pg_snapshot_size(self._h, ctypes.byref(n)))
+        buf = np.empty(max(n.value, 1), dtype=np.uint8)
+        self._check(_lib.lib().p2pg_snapshot(self._h, _lib.ptr(buf), n.value))
+        return buf[:n.value]
+
+    def restore(self, buf):
+        """Continue from a snapshot of an engine with the same configuration, graph and
+        sources (call broadcast(sources) first)."""
+        b = np.ascontiguousarray(buf, dtype=np.uint8)
+        self._check(_lib.lib().p2pg_restore(self._h, _lib.ptr(b), len(b)))
+        self.rounds = []
+        self.message_count_send = int(np.frombuffer(b[:128].tobytes(), dtype=np.uint64)[
+            _SNAP_TOTAL_RELAYS_WORD])
+
+    def save_snapshot(self, path):
+        np.save(path, self.snapshot(), allow_pickle=False)
+
+    def load_snapshot(self, path):
+        self.restore(np.load(path, allow_pickle=False))
 
     # -- the batched hook (override like Node.node_message, node.py:334-338) --------------
     def node_message_batch(self, deliveries):

@@ -27,7 +27,11 @@ send_to_node has counted it -- like a send on a broken connection (nodeconnectio
 Also recorded: config 1 -- 10 real reference Nodes on localhost TCP (ring + chords), one
 flood broadcast with the same dedup app; only reachability and relay count are timing-free.
 
-Usage:  python tests/golden/make_golden.py      (writes tests/golden/*.npz)
+Also: connection changes between rounds (dyn_* fixtures) through the reference's own
+Node.disconnect_with_node / node_disconnected and new NodeConnection pairs.
+
+Usage:  python tests/golden/make_golden.py        (writes tests/golden/*.npz)
+        python tests/golden/make_golden.py dyn    (only the dyn_* fixtures)
 """
 import os
 import sys
@@ -146,12 +150,47 @@ class Harness:
         for v in range(V):
             self.nodes[v].by_peer = sorted(self.nodes[v].all_nodes, key=lambda c: int(c.id))
 
+    def connect(self, a, b):
+        """A new connection, dialled by the lower id (node.py:161 outbound, :251 inbound)."""
+        a, b = min(a, b), max(a, b)
+        ca = NodeConnection(self.nodes[a], FakeSock(self, a, b), str(b), "127.0.0.1", 30000 + b)
+        cb = NodeConnection(self.nodes[b], FakeSock(self, b, a), str(a), "127.0.0.1", 30000 + a)
+        self.nodes[a].nodes_outbound.append(ca)
+        self.nodes[b].nodes_inbound.append(cb)
+        self.conn[(a, b)] = ca
+        self.conn[(b, a)] = cb
+
+    def disconnect(self, a, b):
+        """The dialler's Node.disconnect_with_node (node.py:178-189: event + NodeConnection.stop),
+        then what both NodeConnection threads do on exit (nodeconnection.py:224-228):
+        Node.node_disconnected removes the connection from the lists (node.py:307-319)."""
+        a, b = min(a, b), max(a, b)
+        ca, cb = self.conn.pop((a, b)), self.conn.pop((b, a))
+        self.nodes[a].disconnect_with_node(ca)
+        cb.stop()
+        self.nodes[a].node_disconnected(ca)
+        self.nodes[b].node_disconnected(cb)
+
+    def apply_update(self, add, remove):
+        """Connection changes between rounds: packets in flight on a removed connection are
+        lost (its reader stopped and dropped the unread buffer, nodeconnection.py:192-228)."""
+        gone = set()
+        for a, b in remove:
+            self.disconnect(int(a), int(b))
+            gone |= {(int(a), int(b)), (int(b), int(a))}
+        self.outbox = [o for o in self.outbox if (o[0], o[1]) not in gone]
+        for a, b in add:
+            self.connect(int(a), int(b))
+        for v in range(len(self.nodes)):
+            self.nodes[v].by_peer = sorted(self.nodes[v].all_nodes, key=lambda c: int(c.id))
+
     def dropped(self, a, b):
         if not self.churn_thr:
             return False
         return bool(philox.churn_dropped(self.round, a, b, self.churn_thr, self.cseed))
 
-    def run(self, src):
+    def run(self, src, updates=None):
+        updates = updates or {}
         V, M = self.g.V, len(src)
         sends = lambda: sum(n.message_count_send for n in self.nodes)  # noqa: E731
         rounds = []
@@ -164,6 +203,8 @@ class Harness:
         rounds.append(sends() - before)
         eot = (0x04).to_bytes(1, "big")
         while self.outbox:
+            if self.round in updates:  # changes after round r, before its packets arrive
+                self.apply_update(*updates[self.round])
             self.round += 1
             batch = sorted(self.outbox)  # (receiver, sender, seq)
             self.outbox = []
@@ -195,19 +236,54 @@ class Harness:
         return hop, parent, np.array(rounds, dtype=np.int64), recv
 
 
-def case(name, graph, M, src_seed, mode="flood", k=3, gseed=0, churn=0.0, cseed=0, src=None):
+def random_updates(graph, rounds, n_change, seed):
+    """Connection changes after the given rounds: n_change existing connections removed and
+    n_change new ones added each time (generator input only; the fixture stores them)."""
+    rng = np.random.default_rng(seed)
+    g = graph
+    out = {}
+    for r in rounds:
+        rows = np.repeat(np.arange(g.V), g.degree())
+        edges = np.stack([rows, g.colidx], axis=1)
+        edges = edges[edges[:, 0] < edges[:, 1]]
+        rem = edges[rng.choice(len(edges), n_change, replace=False)]
+        have = set(map(tuple, edges.tolist()))
+        add = []
+        while len(add) < n_change:
+            a, b = sorted(int(x) for x in rng.integers(0, g.V, 2))
+            if a != b and (a, b) not in have and [a, b] not in add:
+                add.append([a, b])
+        add = np.array(add, dtype=np.int32)
+        out[int(r)] = (add, rem.astype(np.int32))
+        g = g.with_changes(add, rem)
+    return out
+
+
+def pack_updates(updates):
+    rounds = np.array(sorted(updates), dtype=np.int64)
+    add = [updates[r][0] for r in rounds]
+    rem = [updates[r][1] for r in rounds]
+    off = lambda xs: np.concatenate([[0], np.cumsum([len(x) for x in xs])]).astype(np.int64)  # noqa: E731
+    cat = lambda xs: np.concatenate(xs).astype(np.int32).reshape(-1, 2) if xs else np.zeros((0, 2), np.int32)  # noqa: E731
+    return dict(upd_rounds=rounds, upd_add=cat(add), upd_add_off=off(add), upd_remove=cat(rem),
+                upd_remove_off=off(rem))
+
+
+def case(name, graph, M, src_seed, mode="flood", k=3, gseed=0, churn=0.0, cseed=0, src=None,
+         updates=None):
     thr = int(np.floor(churn * 4294967296.0)) if churn else 0
     if src is None:
         src = make_sources(graph.V, M, seed=src_seed)
     src = np.asarray(src, dtype=np.int32)
     t = time.time()
-    hop, parent, relays, recv = Harness(graph, mode, k, gseed, thr, cseed).run(src)
+    hop, parent, relays, recv = Harness(graph, mode, k, gseed, thr, cseed).run(src, updates)
     dt = time.time() - t
     out = os.path.join(HERE, f"{name}.npz")
+    extra = pack_updates(updates) if updates else {}
     np.savez_compressed(out, rowptr=graph.rowptr, colidx=graph.colidx, src=src, hop=hop,
                         parent=parent, round_relays=relays, total_recv=np.int64(recv),
                         mode=np.array(mode), fanout=np.int64(k), gossip_seed=np.uint64(gseed),
-                        churn_threshold=np.uint64(thr), churn_seed=np.uint64(cseed))
+                        churn_threshold=np.uint64(thr), churn_seed=np.uint64(cseed), **extra)
     print(f"{name}: V={graph.V} E={graph.n_edges} M={len(src)} mode={mode} rounds={len(relays)} "
           f"relays={relays.sum()} delivered={(hop >= 0).sum()} ({dt:.1f}s, "
           f"{relays.sum() / dt:.0f} relays/s) -> {os.path.getsize(out)} B")
@@ -259,9 +335,28 @@ def config1_tcp():
     print(f"config1_tcp: reached {reached.sum()}/10, relays={relays}, last receipt {last * 1e3:.2f} ms")
 
 
+def dynamic_cases():
+    """Connection changes between rounds, through the reference's own
+    disconnect_with_node / node_disconnected and new NodeConnection pairs."""
+    g = PeerGraph.random_regular(300, 6, seed=21)
+    case("dyn_rrg300_flood", g, 64, src_seed=21, updates=random_updates(g, [0, 1, 2], 40, 1))
+    g = PeerGraph.watts_strogatz(400, 6, 0.1, seed=22)
+    case("dyn_ws400_flood_churn05", g, 96, src_seed=22, churn=0.05, cseed=13,
+         updates=random_updates(g, [1, 3], 60, 2))
+    g = PeerGraph.barabasi_albert(500, 3, seed=23)
+    case("dyn_ba500_gossip_k3", g, 64, src_seed=23, mode="gossip", k=3, gseed=31,
+         updates=random_updates(g, [0, 2, 3], 50, 3))
+    g = PeerGraph.barabasi_albert(400, 4, seed=24)
+    case("dyn_ba400_gossip_k2_churn10", g, 128, src_seed=24, mode="gossip", k=2, gseed=77,
+         churn=0.10, cseed=9, updates=random_updates(g, [1, 4], 40, 4))
+
+
 def main():
     global Node, NodeConnection
     Node, NodeConnection = _load_reference()
+    if sys.argv[1:] == ["dyn"]:
+        dynamic_cases()
+        return
     # config 2: 1k-peer random 8-regular, 64 concurrent floods
     g2 = PeerGraph.random_regular(1000, 8, seed=1)
     case("c2_rrg1000_flood", g2, 64, src_seed=1)
@@ -287,6 +382,7 @@ def main():
     srcs = np.array([0, 9, 10, 29, 35, 30] * 11 + [39, 5, 5, 12], dtype=np.int32)[:70]
     case("edge_components_m70", ge, 70, 0, src=srcs)
     case("edge_components_gossip_k1", ge, 70, 0, src=srcs, mode="gossip", k=1, gseed=3)
+    dynamic_cases()
     config1_tcp()
 
 

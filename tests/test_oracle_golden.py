@@ -5,17 +5,18 @@ Node.message_count_send, p2pnetwork/node.py:116)."""
 import numpy as np
 import pytest
 
-from conftest import golden_cases, load_golden, trim_zeros
+from conftest import golden_cases, load_golden, trim_zeros, updates_of
 from oracle import relay_oracle
 
 
-def run_oracle(z):
+def run_oracle(z, updates=None):
     mode = str(z["mode"])
     if mode == "flood":
         return relay_oracle.flood(z["rowptr"], z["colidx"], z["src"], int(z["churn_threshold"]),
-                                  int(z["churn_seed"]))
+                                  int(z["churn_seed"]), updates=updates)
     return relay_oracle.gossip(z["rowptr"], z["colidx"], z["src"], int(z["fanout"]),
-                               int(z["gossip_seed"]), 0, int(z["churn_threshold"]), int(z["churn_seed"]))
+                               int(z["gossip_seed"]), 0, int(z["churn_threshold"]), int(z["churn_seed"]),
+                               updates=updates)
 
 
 @pytest.mark.parametrize("name", golden_cases())
@@ -30,6 +31,34 @@ def test_oracle_matches_reference_harness(name):
     hop = z["hop"]
     for r in res.rounds:
         assert r["new_deliveries"] == int((hop == r["round"]).sum())
+
+
+@pytest.mark.parametrize("name", golden_cases(dynamic=True))
+def test_oracle_dynamic_topology_matches_reference_harness(name):
+    """Connection changes between rounds, driven through the reference's own
+    disconnect_with_node / node_disconnected and new NodeConnection pairs: in-flight packets
+    on removed connections are lost, later sends use the new connections."""
+    z = load_golden(name)
+    res = run_oracle(z, updates_of(z))
+    np.testing.assert_array_equal(res.hop, z["hop"])
+    np.testing.assert_array_equal(res.parent, z["parent"])
+    relays = [r["relays"] for r in res.rounds]
+    np.testing.assert_array_equal(trim_zeros(relays), trim_zeros(z["round_relays"]))
+    # the changes do matter: without them the results differ
+    assert not np.array_equal(run_oracle(z).hop, z["hop"])
+
+
+def test_peergraph_with_changes_matches_oracle():
+    """GraphNetwork's host-side topology bookkeeping == the oracle's CSR update."""
+    from p2pnetwork.gpu.graph import PeerGraph
+    z = load_golden("dyn_rrg300_flood")
+    g = PeerGraph(z["rowptr"], z["colidx"])
+    rp, ci = z["rowptr"], z["colidx"].astype(np.int64)
+    for r, (a, d) in sorted(updates_of(z).items()):
+        g = g.with_changes(a, d)
+        rp, ci = relay_oracle._apply_changes(rp, ci, a, d)
+        np.testing.assert_array_equal(g.rowptr, rp)
+        np.testing.assert_array_equal(g.colidx, ci)
 
 
 def test_config2_relay_identity():
