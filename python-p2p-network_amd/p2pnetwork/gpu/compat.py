@@ -39,6 +39,10 @@ Semantics (compat mode):
   semantics: every attempted send, also those churn drops); ``message_count_recv`` = its
   deliveries (first receipts -- duplicates are dropped by the engine before any hook).
 * Lifecycle: ``start`` / ``join`` are no-ops; ``stop`` fires ``node_request_to_stop``.
+* Connection changes: ``connect_with_node(host, port)`` / ``disconnect_with_node(conn)`` (also
+  from inside ``node_message``) take effect between rounds through the engine's
+  ``update_edges``: connected events fire then; a removed connection loses the messages in
+  flight on it and both ends get ``node_disconnected`` (node.py:122-189, :307-319).
 """
 import hashlib
 import random
@@ -142,10 +146,31 @@ class SimNode:
         self.terminate_flag.set()
 
     def connect_with_node(self, host, port, reconnect=False):
-        raise NotImplementedError("compat mode: the topology is the PeerGraph given to CompatNetwork")
+        """Dial another simulated node (node.py:122-176): self connections are refused, an
+        existing connection is reported; the new connection exists from the next round on
+        (its connected events fire then, like the reference's asynchronous handshake)."""
+        if host == self.host and port == self.port:
+            print("connect_with_node: Cannot connect with yourself!!")
+            return False
+        peer = self._net._peer_at(host, port)
+        if peer is None:
+            self.outbound_node_connection_error(ConnectionRefusedError(f"{host}:{port}"))
+            return False
+        if peer in self._net._conn[self._peer] or self._net._queued(self._peer, peer, True):
+            self.debug_print(f"connect_with_node: Already connected with this node ({host}:{port}).")
+            return True
+        self._net._queue_change(self._peer, peer, True)
+        return True
 
     def disconnect_with_node(self, node):
-        raise NotImplementedError("compat mode: the topology is fixed for a run")
+        """Close one of our outbound connections (node.py:178-189); it goes away between rounds
+        -- messages in flight on it are lost -- and both ends see node_disconnected."""
+        if node in self.nodes_outbound:
+            self.node_disconnect_with_outbound_node(node)
+            node.stop()
+            self._net._queue_change(self._peer, node.peer, False)
+        else:
+            self.debug_print("Node disconnect_with_node: cannot disconnect with a node with which we are not connected.")
 
     # -- event hooks (node.py:282-363), identical callback dispatch ----------------------------
     def outbound_node_connected(self, node):
@@ -241,6 +266,8 @@ class CompatNetwork:
                 na.outbound_node_connected(ca)
                 nb.inbound_node_connected(cb)
         self._deg = graph.degree()
+        self._by_addr = {(n.host, n.port): v for v, n in enumerate(self.nodes)}
+        self._changes = []  # (a, b, connect) queued by connect_with_node / disconnect_with_node
         make = engine_factory or GraphNetwork
         self.engine = make(graph, mode=mode, fanout=fanout, **engine_kw)
         self.origins, self.payloads = [], []
@@ -277,10 +304,47 @@ class CompatNetwork:
     def _conn_send(self, node, conn, data, compression):
         self._send_to_node(node, conn, data, compression)
 
+    # -- connection changes (applied between rounds) -----------------------------------------
+    def _peer_at(self, host, port):
+        return self._by_addr.get((host, port))
+
+    def _queued(self, a, b, connect):
+        return any({x, y} == {a, b} and c == connect for x, y, c in self._changes)
+
+    def _queue_change(self, a, b, connect):
+        self._changes.append((int(a), int(b), bool(connect)))
+
+    def _apply_changes(self):
+        """Hand the queued changes to the engine (p2pg_update_edges) and mirror them on the
+        node objects: new SimConnections + connected events (dialler outbound, other end
+        inbound), removed ones + node_disconnected on both ends (node.py:307-319)."""
+        if not self._changes:
+            return
+        changes, self._changes = self._changes, []
+        add = [(a, b) for a, b, c in changes if c]
+        rem = [(a, b) for a, b, c in changes if not c]
+        self.engine.update_edges(add=add, remove=rem)
+        self.graph = self.engine.graph
+        self._deg = self.graph.degree()
+        for a, b in rem:
+            ca, cb = self._conn[a].pop(b), self._conn[b].pop(a)
+            self.nodes[a].node_disconnected(ca)
+            self.nodes[b].node_disconnected(cb)
+        for a, b in add:
+            na, nb = self.nodes[a], self.nodes[b]
+            ca = SimConnection(na, b, nb.id, nb.host, nb.port)
+            cb = SimConnection(nb, a, na.id, na.host, na.port)
+            na.nodes_outbound.append(ca)
+            nb.nodes_inbound.append(cb)
+            self._conn[a][b], self._conn[b][a] = ca, cb
+            na.outbound_node_connected(ca)
+            nb.inbound_node_connected(cb)
+
     # -- running ------------------------------------------------------------------------------
     def run(self, max_rounds=1 << 20):
         """Relay every broadcast originated so far to quiescence, dispatching hooks per round.
         Returns the engine's per-round stats."""
+        self._apply_changes()  # changes made before the run: the starting topology
         if not self.origins:
             return []
         src = np.asarray(self.origins, dtype=np.int32)
@@ -296,9 +360,15 @@ class CompatNetwork:
                 order = np.lexsort((d.msg, d.peer))
                 for i in order:
                     self._deliver(int(d.peer[i]), int(d.msg[i]), int(d.parent[i]), st.round, k)
+            self.between_rounds(st.round)
+            self._apply_changes()  # made by the hooks of this round: effective from the next
             if not st.active:
                 break
         return out
+
+    def between_rounds(self, rnd):
+        """Called after round rnd's node_message calls, before queued connection changes are
+        applied (override to drive topology changes from outside the nodes)."""
 
     def _deliver(self, v, m, parent, rnd, k):
         node = self.nodes[v]

@@ -6,7 +6,7 @@ test-only engine stand-in (tests/partition_mock.py); the gpu-marked ones with th
 import numpy as np
 import pytest
 
-from conftest import golden_cases, load_golden
+from conftest import golden_cases, load_golden, updates_of
 from partition_mock import MockEngine
 
 
@@ -105,3 +105,56 @@ def test_compat_gpu_engine_matches_reference_golden(name):
     hop, par, sends, recv, net = run_compat(z)
     check(z, hop, par, sends, recv)
     assert net.absorbed_sends == recv if str(z["mode"]) == "flood" else True
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", golden_cases(dynamic=True))
+def test_compat_gpu_connection_changes_match_reference_golden(name):
+    """Node-style connect_with_node / disconnect_with_node between rounds (the dialler is the
+    lower id, as in the reference harness) reproduce the dyn_* fixtures; the lifecycle events
+    fire on both ends."""
+    from p2pnetwork.gpu import PeerGraph
+    from p2pnetwork.gpu.compat import CompatNetwork
+    z = load_golden(name)
+    upd = updates_of(z)
+    events = []
+
+    class Net(CompatNetwork):
+        def between_rounds(self, rnd):
+            if rnd not in upd:
+                return
+            add, rem = upd[rnd]
+            for a, b in rem:
+                a, b = sorted((int(a), int(b)))
+                self.nodes[a].disconnect_with_node(self._conn[a][b])
+            for a, b in add:
+                a, b = sorted((int(a), int(b)))
+                assert self.nodes[a].connect_with_node(self.nodes[b].host, self.nodes[b].port)
+
+    def cb(event, main_node, connected_node, data):
+        if event != "node_message":
+            events.append(event)
+
+    App = dedup_app()
+    g = PeerGraph(z["rowptr"], z["colidx"])
+    net = Net(g, App, mode=str(z["mode"]), fanout=int(z["fanout"]), gossip_seed=int(z["gossip_seed"]),
+              churn_threshold_value=int(z["churn_threshold"]), churn_seed=int(z["churn_seed"]),
+              node_kwargs={"callback": cb})
+    events.clear()
+    for m, s in enumerate(z["src"]):
+        net.nodes[int(s)].seen[m] = (0, -1)
+        net.nodes[int(s)].send_to_nodes({"mid": m})
+    net.run()
+    V, M = g.V, len(z["src"])
+    hop = np.full((V, M), -1, np.int32)
+    par = np.full((V, M), -1, np.int32)
+    for v, n in enumerate(net.nodes):
+        for m, (h, p) in n.seen.items():
+            hop[v, m], par[v, m] = h, p
+    check(z, hop, par, sum(n.message_count_send for n in net.nodes), sum(n.message_count_recv for n in net.nodes))
+    n_add = sum(len(a) for a, _ in upd.values())
+    n_rem = sum(len(r) for _, r in upd.values())
+    assert events.count("outbound_node_connected") == events.count("inbound_node_connected") == n_add
+    assert events.count("outbound_node_disconnected") == events.count("inbound_node_disconnected") == n_rem
+    assert events.count("node_disconnect_with_outbound_node") == n_rem
+    net.close()
