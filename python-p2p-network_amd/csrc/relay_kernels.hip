@@ -884,7 +884,7 @@ __device__ __forceinline__ void scatter_row(const DevGraph& g, const DevState& s
 }
 
 // The scatter launch: tasks [task0, nwords) are 32-peer bitmap words (sources with deg <=
-// GCHUNK), tasks [nwords, nwords + n_hub) are (wide source, chunk) items.  task0 = nwords
+// GCHUNK), tasks from nwords on are groups of 64 (wide source, chunk) items.  task0 = nwords
 // runs the items only (fused rounds: the items of the pull hubs, deg > HUB_T).
 template <bool CHURN, int K, bool STORE_E>
 __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st, RoundParams p,
@@ -899,7 +899,7 @@ __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st,
   const int cur = p.round & 1;
   const uint64_t* __restrict__ Fc = st.F[cur];
   const int64_t nwords = (V + 31) >> 5;
-  const int64_t ntasks = nwords + n_hub;
+  const int64_t ntasks = nwords + ((n_hub + 63) >> 6);
   const int nslices = (W + 63) >> 6;
   uint64_t c[STAT_N] = {0, 0, 0, 0, 0, 0, 0, 0};
   PROF_DECL  // development builds: segment clocks of this kernel are not reported
@@ -957,26 +957,9 @@ __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st,
       }
       continue;
     }
-    uint32_t todo;
-    int64_t base;
-    int chunk;
-    if (task < nwords) {
-      todo = st.A[cur][task];
-      base = task << 5;
-      chunk = 0;
-    } else {
-      const int64_t it = hub_items[task - nwords];
-      base = it >> 32;
-      chunk = (int)(it & 0xFFFFFFFFll);
-      todo = bit_test(st.A[cur], base) ? 1u : 0u;
-    }
-    while (todo) {
-      const int b = __builtin_ctz(todo);
-      todo &= todo - 1u;
-      const int64_t v = task < nwords ? base + b : base;
+    auto one_source = [&](int64_t v, int chunk) {
       const int64_t rb = g.rowptr[v];
       const int64_t deg = g.rowptr[v + 1] - rb;
-      if (task < nwords && deg > GCHUNK) continue;  // hub: handled by its chunk items
       const int nb = chunk * GCHUNK;
       const int nn = (int)(deg - nb < GCHUNK ? deg - nb : GCHUNK);
       const uint32_t rv = load_nbr(rb + nb, nn);
@@ -985,6 +968,34 @@ __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st,
         const uint64_t f = w < W ? Fc[v * W + w] : 0ull;
         scatter_row<CHURN, K, STORE_E>(g, st, p, L, lane, v, rb, deg, chunk, sl, f, rv, 0, c PROF_PASS);
       }
+    };
+    if (task < nwords) {  // multi-slice rows (W > 64)
+      uint32_t todo = st.A[cur][task];
+      while (todo) {
+        const int b = __builtin_ctz(todo);
+        todo &= todo - 1u;
+        const int64_t v = (task << 5) + b;
+        if (g.rowptr[v + 1] - g.rowptr[v] > GCHUNK) continue;  // wide: its chunk items
+        one_source(v, 0);
+      }
+      continue;
+    }
+    // 64 (wide source, chunk) items per task, their activity tested lane-parallel: in sparse
+    // rounds almost every item is skipped, and one dependent load chain per item would make
+    // an idle launch cost ~0.3 ms (config 4 has ~1.4M items)
+    const int64_t i = (task - nwords) * 64 + lane;
+    int64_t item = 0;
+    bool act = false;
+    if (i < n_hub) {
+      item = hub_items[i];
+      act = bit_test(st.A[cur], item >> 32);
+    }
+    uint64_t am = __ballot(act);
+    while (am) {
+      const int l = __builtin_ctzll(am);
+      am &= am - 1ull;
+      const int64_t it = readlane64(item, l);
+      one_source(it >> 32, (int)(it & 0xFFFFFFFFll));
     }
   }
   flush_stats(st.stats, c, lane);
@@ -1474,6 +1485,21 @@ int grid_tasks(int64_t ntasks) {
   return (int)(b < 1 ? 1 : (b > cap ? cap : b));
 }
 
+// Grid for the per-peer pull kernels, whose task cost is very uneven (power-law degrees,
+// receipts per peer): P2PG_FUSED_GRID (default 32) x the blocks resident at once, so that
+// blocks finishing early are replaced (measured on config 4: 2x -> 300 ms, 8x -> 267 ms,
+// 32x -> 260 ms for the fused rounds).
+template <class F>
+int balanced_grid(F kernel, int64_t ntasks) {
+  static const int gmul = [] {
+    const char* e = std::getenv("P2PG_FUSED_GRID");
+    const int v = e ? std::atoi(e) : 32;
+    return v > 0 ? v : 32;
+  }();
+  return (int)std::min<int64_t>((int64_t)grid_tasks_uncapped(ntasks),
+                                (int64_t)gmul * resident_blocks(kernel));
+}
+
 }  // namespace
 
 hipError_t launch_zero_rows(uint64_t* plane, int32_t W, const int32_t* rows, int32_t n,
@@ -1499,7 +1525,9 @@ hipError_t pull_with_hubs(const DevGraph& g, const DevState& st, const RoundPara
     if (hp.n_items)
       hipLaunchKernelGGL((k_pull_hub_partial<CHURN, GOSSIP>), dim3(grid_tasks(hp.n_items)),
                          dim3(256), 0, s, g, st, p, hp);
-    hipLaunchKernelGGL((k_pull1<CHURN, GOSSIP>), dim3(grid), dim3(256), 0, s, g, st, p);
+    hipLaunchKernelGGL((k_pull1<CHURN, GOSSIP>),
+                       dim3(balanced_grid(k_pull1<CHURN, GOSSIP>, (g.V + 31) >> 5)), dim3(256), 0,
+                       s, g, st, p);
     if (hp.n_hubs)
       hipLaunchKernelGGL((k_pull_hub_finalize<GOSSIP>), dim3(grid_tasks(hp.n_hubs)), dim3(256),
                          0, s, g, st, p, hp);
@@ -1560,7 +1588,7 @@ void scatter_dispatch(int grid, const DevGraph& g, const DevState& st, const Rou
 hipError_t launch_gossip_scatter(const DevGraph& g, const DevState& st, const RoundParams& p,
                                  const int64_t* hub_items, int64_t n_hub_items, bool store_e,
                                  hipStream_t s) {
-  const int grid = grid_tasks(((g.V + 31) >> 5) + n_hub_items);
+  const int grid = grid_tasks(((g.V + 31) >> 5) + ((n_hub_items + 63) >> 6));
   if (store_e)
     scatter_dispatch<true>(grid, g, st, p, hub_items, n_hub_items, 0, s);
   else
@@ -1576,19 +1604,10 @@ hipError_t launch_gossip_fused(const DevGraph& g, const DevState& st, const Roun
   if (hp.n_items)
     hipLaunchKernelGGL((k_pull_hub_partial<false, true>), dim3(grid_tasks(hp.n_items)),
                        dim3(256), 0, s, g, st, p, hp);
-  // grid = P2PG_FUSED_GRID x the blocks resident at once (default 32, measured: 2 -> 300 ms,
-  // 8 -> 267 ms, 32 -> 260 ms per config-4 step): blocks that finish early are replaced,
-  // which evens out the very uneven per-task cost (hubs, receipts per peer)
-  static const int gmul = [] {
-    const char* e = std::getenv("P2PG_FUSED_GRID");
-    const int v = e ? std::atoi(e) : 32;
-    return v > 0 ? v : 32;
-  }();
-#define P2PG_FUSED(CH, KK)                                                                     \
-  hipLaunchKernelGGL((k_gossip_fused<CH, KK>),                                               \
-                     dim3(std::min<int64_t>((int64_t)grid_tasks_uncapped((g.V + 31) >> 5),    \
-                                            (int64_t)gmul * resident_blocks(k_gossip_fused<CH, KK>))), \
-                     dim3(256), 0, s, g, st, p)
+#define P2PG_FUSED(CH, KK)                                                                   \
+  hipLaunchKernelGGL((k_gossip_fused<CH, KK>),                                             \
+                     dim3(balanced_grid(k_gossip_fused<CH, KK>, (g.V + 31) >> 5)), dim3(256), 0, \
+                     s, g, st, p)
   const bool ch = p.churn_thr != 0;
   switch (p.fanout) {
     case 1: if (ch) P2PG_FUSED(true, 1); else P2PG_FUSED(false, 1); break;
@@ -1603,7 +1622,7 @@ hipError_t launch_gossip_fused(const DevGraph& g, const DevState& st, const Roun
                        s, g, st, p, hp);
   if (n_big) {
     const int64_t nwords = (g.V + 31) >> 5;
-    scatter_dispatch<true>(grid_tasks(n_big), g, st, p, big_items, n_big, nwords, s);
+    scatter_dispatch<true>(grid_tasks((n_big + 63) >> 6), g, st, p, big_items, n_big, nwords, s);
   }
   return hipGetLastError();
 }
