@@ -65,6 +65,17 @@ __device__ __forceinline__ uint32_t wave_reduce_u32(uint32_t x) {
   return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
 }
 
+// Inclusive prefix sum over the wave (the same DPP steps as wave_reduce_u32<false>).
+__device__ __forceinline__ uint32_t wave_scan_u32(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);
+  return x;
+}
+
 __device__ __forceinline__ void flush_stats(unsigned long long* stats, const uint64_t* c,
                                             int lane) {
   unsigned long long* shard = stats + (blockIdx.x & (STAT_SHARDS - 1)) * STAT_N;
@@ -716,6 +727,10 @@ __device__ __forceinline__ void wave_lds_sync() {
 #define PROF_PASS
 #endif
 
+#ifndef P2PG_PICK_PAIRS
+#define P2PG_PICK_PAIRS 0
+#endif
+
 // LDS of one scatter wave: a GCHUNK x 64-word mask table (two 32-bit halves per word, so
 // 32-bit LDS atomics) and the compacted list of active (word, bit) entries.
 struct ScatterLds {
@@ -765,7 +780,7 @@ __device__ __forceinline__ void scatter_row(const DevGraph& g, const DevState& s
   // Philox + Floyd for list entries [0, n) of this wave, picks ORed into the LDS table.
   auto pick_batch = [&](auto check_v, uint32_t n) {
     constexpr bool CHECK = decltype(check_v)::value;
-    auto one = [&](uint32_t e) {
+    auto one = [&](uint32_t e, bool ok) {
       const uint32_t wl = e >> 6, bit = e & 63u;
       const uint32_t mg = p.msg_base + (uint32_t)((sl * 64 + (int)wl) * 64) + bit;
       uint32_t* const col = &L.tbl[0][bit >> 5][wl];
@@ -776,16 +791,35 @@ __device__ __forceinline__ void scatter_row(const DevGraph& g, const DevState& s
 #pragma unroll
       for (int q = 0; q < (K > 0 ? K : 1); ++q) {
         const uint32_t jj = pk[q] - (uint32_t)nb;
-        if (!CHECK || jj < (uint32_t)nn) atomicOr(col + jj * 128u, mb);
+        if (ok && (!CHECK || jj < (uint32_t)nn)) atomicOr(col + jj * 128u, mb);
       }
     };
-    // the next batch's list entry is read before this batch's Philox (hides the LDS trip)
-    uint32_t en = (uint32_t)lane < n ? L.lst[lane] : 0u;
-    for (uint32_t i = lane; i < n; i += 64) {
-      const uint32_t e = en;
-      en = i + 64 < n ? L.lst[i + 64] : 0u;
-      one(e);
+    // Strided: in batch b lane l takes entry l*nbat + b.  The list is word-major (a word's
+    // bits are adjacent), so the 64 entries of a batch come from ~64 different words, i.e.
+    // their table atomics hit different LDS banks.  The next batch's entry is read before this
+    // batch's Philox (hides the LDS trip).
+    const uint32_t nbat = (n + 63) >> 6;
+    const uint32_t i0 = (uint32_t)lane * nbat;
+    const uint32_t cnt = i0 < n ? (n - i0 < nbat ? n - i0 : nbat) : 0u;
+#if P2PG_PICK_PAIRS
+    // two entries per iteration, evaluated unconditionally (the second's atomics masked when
+    // past the lane's share): two independent Philox chains interleave and hide each other's
+    // multiply latency
+    for (uint32_t b = 0; b < cnt; b += 2) {
+      const uint32_t e0 = L.lst[i0 + b];
+      const bool two = b + 1 < cnt;
+      const uint32_t e1 = two ? L.lst[i0 + b + 1] : e0;
+      one(e0, true);
+      one(e1, two);
     }
+#else
+    uint32_t en = cnt ? L.lst[i0] : 0u;
+    for (uint32_t b = 0; b < cnt; ++b) {
+      const uint32_t e = en;
+      en = b + 1 < cnt ? L.lst[i0 + b + 1] : 0u;
+      one(e, true);
+    }
+#endif
   };
 
   if (anyf && !all) {
@@ -793,28 +827,21 @@ __device__ __forceinline__ void scatter_row(const DevGraph& g, const DevState& s
       L.tbl[j][0][lane] = 0u;
       L.tbl[j][1][lane] = 0u;
     }
-    // rank-major compaction: list = every word's 1st set bit, then every word's 2nd set
-    // bit, ... so a 64-entry batch covers ~64 distinct words (distinct LDS banks), while
-    // every lane still gets equal Philox work
+    // word-major compaction: lane w lists its word's set bits at its exclusive prefix-sum
+    // position (one DPP scan; a 32-bit ctz / clear per bit), so every lane gets an equal
+    // share of the Philox work; pick_batch reads the list strided (distinct words per batch)
     const uint32_t cnt = (uint32_t)__popcll(f);
-    const uint32_t maxc = wave_reduce_u32<true>(cnt);
-    const uint32_t total = wave_reduce_u32<false>(cnt);
+    const uint32_t incl = wave_scan_u32(cnt);
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    const uint32_t pos0 = incl - cnt;
     for (uint32_t lb = 0; lb < total; lb += GLIST) {
-      uint64_t ff = f;
-      uint32_t base = 0;
-      for (uint32_t kr = 0; kr < maxc; ++kr) {
-        const bool has = cnt > kr;
-        const uint64_t mk = __ballot(has);
-        if (has) {
-          const uint32_t pos =
-              base + __builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32),
-                                               __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
-          const int bit = __builtin_ctzll(ff);
-          ff &= ff - 1ull;
-          if (pos >= lb && pos < lb + GLIST) L.lst[pos - lb] = (uint16_t)((lane << 6) | bit);
-        }
-        base += (uint32_t)__popcll(mk);
-      }
+      const uint32_t nw = total - lb < (uint32_t)GLIST ? total - lb : (uint32_t)GLIST;
+      uint32_t li = pos0 - lb;  // list index of this lane's next bit (wraps below the pass)
+      const uint32_t hi_tag = ((uint32_t)lane << 6) | 32u;
+      for (uint32_t h = (uint32_t)f; h; h &= h - 1u, ++li)
+        if (li < nw) L.lst[li] = (uint16_t)(((uint32_t)lane << 6) | (uint32_t)__builtin_ctz(h));
+      for (uint32_t h = (uint32_t)(f >> 32); h; h &= h - 1u, ++li)
+        if (li < nw) L.lst[li] = (uint16_t)(hi_tag | (uint32_t)__builtin_ctz(h));
       wave_lds_sync();
       PROF_MARK(6);
       const uint32_t n = total - lb < (uint32_t)GLIST ? total - lb : (uint32_t)GLIST;
@@ -1600,7 +1627,6 @@ hipError_t launch_gossip_fused(const DevGraph& g, const DevState& st, const Roun
                                const HubPlan& hp, const int64_t* big_items, int64_t n_big,
                                hipStream_t s) {
   if (st.W > 64 || !st.AW[0] || st.E[0] == st.E[1]) return hipErrorInvalidValue;
-  const int grid = grid_tasks((g.V + 31) >> 5);
   if (hp.n_items)
     hipLaunchKernelGGL((k_pull_hub_partial<false, true>), dim3(grid_tasks(hp.n_items)),
                        dim3(256), 0, s, g, st, p, hp);
