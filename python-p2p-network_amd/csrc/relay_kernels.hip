@@ -1615,7 +1615,14 @@ void scatter_dispatch(int grid, const DevGraph& g, const DevState& st, const Rou
 hipError_t launch_gossip_scatter(const DevGraph& g, const DevState& st, const RoundParams& p,
                                  const int64_t* hub_items, int64_t n_hub_items, bool store_e,
                                  hipStream_t s) {
-  const int grid = grid_tasks(((g.V + 31) >> 5) + ((n_hub_items + 63) >> 6));
+  // blocks cap: P2PG_SCATTER_GRID (default GRID_MAX)
+  static const int64_t cap = [] {
+    const char* e = std::getenv("P2PG_SCATTER_GRID");
+    const int64_t v = e ? std::atoll(e) : GRID_MAX;
+    return v > 0 ? v : (int64_t)GRID_MAX;
+  }();
+  const int grid = (int)std::min<int64_t>(
+      grid_tasks_uncapped(((g.V + 31) >> 5) + ((n_hub_items + 63) >> 6)), cap);
   if (store_e)
     scatter_dispatch<true>(grid, g, st, p, hub_items, n_hub_items, 0, s);
   else
