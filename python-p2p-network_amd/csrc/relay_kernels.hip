@@ -730,6 +730,9 @@ __device__ __forceinline__ void wave_lds_sync() {
 #ifndef P2PG_PICK_PAIRS
 #define P2PG_PICK_PAIRS 0
 #endif
+#ifndef P2PG_COMPACT
+#define P2PG_COMPACT 1
+#endif
 
 // LDS of one scatter wave: a GCHUNK x 64-word mask table (two 32-bit halves per word, so
 // 32-bit LDS atomics) and the compacted list of active (word, bit) entries.
@@ -822,10 +825,44 @@ __device__ __forceinline__ void scatter_row(const DevGraph& g, const DevState& s
 #endif
   };
 
-  if (anyf && !all) {
-    for (int j = 0; j < nn; ++j) {
-      L.tbl[j][0][lane] = 0u;
-      L.tbl[j][1][lane] = 0u;
+  // Compact table clear and flush (few active words, no churn): the nf <= 32 active words of
+  // the slice are ranked (rank = position in the packed E row) and lane l serves rank
+  // l % seg of connection l / seg, so one LDS / store / atomic instruction covers 64 / seg
+  // connections instead of one (light dense rounds: ~8 active words, 4 connections at once).
+  // The picks touch only the active words' table columns, so only those are cleared.
+  const int nf = __popcll(fam);
+  const bool compact = P2PG_COMPACT && !CHURN && anyf && nf <= 32 &&
+                       (STORE_E ? st.AW[cur] != nullptr : g.gone == nullptr);
+  const bool use_tbl = anyf && !all;
+  int seg = 64, rk_lane = 0, wc = 0, gl = 0;
+  bool rk = false;
+  if (compact) {
+    seg = nf <= 16 ? 16 : 32;
+    const int rank = (int)__builtin_amdgcn_mbcnt_hi(
+        (uint32_t)(fam >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fam, 0u));
+    // every active word pushes its index to lane `rank`; the others to lane 63 (never read)
+    const int wr = __builtin_amdgcn_ds_permute((f ? rank : 63) << 2, lane);
+    rk_lane = lane & (seg - 1);
+    wc = __builtin_amdgcn_ds_bpermute(rk_lane << 2, wr);  // the word of rank rk_lane
+    rk = rk_lane < nf;
+    gl = lane / seg;
+  }
+  const int gper = 64 / seg;
+
+  if (use_tbl) {
+    if (compact) {
+      for (int j0 = 0; j0 < nn; j0 += gper) {
+        const int jj = j0 + gl;
+        if (rk && jj < nn) {
+          L.tbl[jj][0][wc] = 0u;
+          L.tbl[jj][1][wc] = 0u;
+        }
+      }
+    } else {
+      for (int j = 0; j < nn; ++j) {
+        L.tbl[j][0][lane] = 0u;
+        L.tbl[j][1][lane] = 0u;
+      }
     }
     // word-major compaction: lane w lists its word's set bits at its exclusive prefix-sum
     // position (one DPP scan; a 32-bit ctz / clear per bit), so every lane gets an equal
@@ -870,7 +907,35 @@ __device__ __forceinline__ void scatter_row(const DevGraph& g, const DevState& s
       PROF_MARK(7);
     }
   }
-  const bool use_tbl = anyf && !all;
+  if (compact) {
+    const uint64_t segm = (1ull << seg) - 1ull;
+    uint64_t fr = 0;
+    if (all) {
+      const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(wc << 2, (int)(uint32_t)f);
+      const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(wc << 2, (int)(uint32_t)(f >> 32));
+      fr = ((uint64_t)hi << 32) | lo;
+    }
+    for (int j0 = 0; j0 < nn; j0 += gper) {
+      const int jj = j0 + gl;
+      const bool ok = rk && jj < nn;
+      uint64_t x = 0;
+      if (ok) x = all ? fr : (((uint64_t)L.tbl[jj][1][wc] << 32) | L.tbl[jj][0][wc]);
+      const uint32_t nj = (uint32_t)__builtin_amdgcn_ds_bpermute(
+          (nbr0 + (jj < nn ? jj : 0)) << 2, (int)nbr);
+      const uint64_t bal = __ballot(ok && x != 0ull);
+      if (STORE_E) {
+        if (ok) Eo[(int64_t)nj * W + rk_lane] = x;
+      } else {
+        const int64_t u = (int64_t)nj;
+        if (x) atomicOr((unsigned long long*)&nx[u * W + sl * 64 + wc], (unsigned long long)x);
+        if (rk_lane == 0 && ((bal >> (lane & ~(seg - 1))) & segm))
+          atomicOr(&Tn[u >> 5], 1u << (u & 31));
+      }
+      if (lane == 0) c[ST_SCATTER] += (CT)__popcll(bal);
+    }
+    PROF_MARK(8);
+    return;
+  }
   auto tbl_row = [&](int j) -> uint64_t {
     return ((uint64_t)L.tbl[j][1][lane] << 32) | L.tbl[j][0][lane];
   };
