@@ -62,7 +62,11 @@ P2PG_HD u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
 
 // Lemire multiply-high reduction of a 32-bit draw onto [0, n).
 P2PG_HD uint32_t lemire32(uint32_t x, uint32_t n) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __umulhi(x, n);  // one v_mul_hi_u32, and a 32-bit value for the Floyd compares
+#else
   return (uint32_t)(((uint64_t)x * (uint64_t)n) >> 32);
+#endif
 }
 
 P2PG_HD uint32_t word_of(const u32x4& r, int i) {

@@ -787,14 +787,14 @@ __device__ __forceinline__ void scatter_row(const DevGraph& g, const DevState& s
       const uint32_t wl = e >> 6, bit = e & 63u;
       const uint32_t mg = p.msg_base + (uint32_t)((sl * 64 + (int)wl) * 64) + bit;
       uint32_t* const col = &L.tbl[0][bit >> 5][wl];
-      const uint32_t mb = 1u << (bit & 31u);
+      const uint32_t mb = ok ? 1u << (bit & 31u) : 0u;
       uint32_t pk[K > 0 ? K : 1];
       gossip_picks_t<(K > 0 ? K : 1)>((uint32_t)p.round, gv, mg, (uint32_t)deg, p.gseed_lo,
                                       p.gseed_hi, pk);
 #pragma unroll
       for (int q = 0; q < (K > 0 ? K : 1); ++q) {
         const uint32_t jj = pk[q] - (uint32_t)nb;
-        if (ok && (!CHECK || jj < (uint32_t)nn)) atomicOr(col + jj * 128u, mb);
+        if (!CHECK || jj < (uint32_t)nn) atomicOr(col + jj * 128u, mb);
       }
     };
     // Strided: in batch b lane l takes entry l*nbat + b.  The list is word-major (a word's
@@ -816,11 +816,14 @@ __device__ __forceinline__ void scatter_row(const DevGraph& g, const DevState& s
       one(e1, two);
     }
 #else
-    uint32_t en = cnt ? L.lst[i0] : 0u;
-    for (uint32_t b = 0; b < cnt; ++b) {
-      const uint32_t e = en;
-      en = b + 1 < cnt ? L.lst[i0 + b + 1] : 0u;
-      one(e, true);
+    // Uniform trip count: a lane past its share evaluates a dummy entry whose table ORs carry
+    // an empty mask, so the loop needs no per-lane exit bookkeeping.  i0 + b + 1 <= GLIST.
+    uint32_t en = L.lst[i0];
+    for (uint32_t b = 0; b < nbat; ++b) {
+      const uint32_t e = en & 0x0FFFu;  // in range even when stale
+      const uint32_t ni = i0 + b + 1;
+      en = L.lst[ni < (uint32_t)GLIST ? ni : (uint32_t)GLIST - 1u];
+      one(e, b < cnt);
     }
 #endif
   };
