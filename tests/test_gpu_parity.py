@@ -241,22 +241,29 @@ def test_config4_gossip_full_size_parity():
     with gpu_net(g, "gossip", 3, 0x5EED, record=False) as net:
         net.broadcast(src)
         a = net.run()
-        word0 = net.seen_plane()[:, 0].copy()
+        seen = net.seen_plane()
+        words = {0: seen[:, 0].copy(), 63: seen[:, 63].copy()}
+        del seen
         net.reset()
         b = net.run()
     assert [r.as_dict() for r in a] == [r.as_dict() for r in b]
     for r in a:
         assert r.relays == 3 * r.new_deliveries
-    with gpu_net(g, "gossip", 3, 0x5EED, record=True) as net:
-        net.broadcast(src[:64])
-        sub = net.run()
-        hop, parent = net.hop_parent()
-    bits = np.unpackbits(word0.view(np.uint8).reshape(g.V, 8), axis=1, bitorder="little").astype(bool)
-    np.testing.assert_array_equal(bits, hop >= 0)
-    ora = coracle.run(g.rowptr, g.colidx, src[:64], "gossip", 3, 0x5EED, record=True)
-    np.testing.assert_array_equal(hop, ora.hop)
-    np.testing.assert_array_equal(parent, ora.parent)
-    assert_rounds_equal(sub, ora.rounds)
+    # word 0 (messages 0..63) and word 63 (4032..4095: the Philox counters carry the global
+    # message id, so a 64-broadcast run with msg_id_base 4032 is the same experiment)
+    for w, word in words.items():
+        base = 64 * w
+        with gpu_net(g, "gossip", 3, 0x5EED, record=True, msg_id_base=base) as net:
+            net.broadcast(src[base:base + 64])
+            sub = net.run()
+            hop, parent = net.hop_parent()
+        bits = np.unpackbits(word.view(np.uint8).reshape(g.V, 8), axis=1, bitorder="little").astype(bool)
+        np.testing.assert_array_equal(bits, hop >= 0)
+        ora = coracle.run(g.rowptr, g.colidx, src[base:base + 64], "gossip", 3, 0x5EED,
+                          msg_id_base=base, record=True)
+        np.testing.assert_array_equal(hop, ora.hop)
+        np.testing.assert_array_equal(parent, ora.parent)
+        assert_rounds_equal(sub, ora.rounds)
 
 
 @pytest.mark.parametrize("push", ["atomic", "store", "auto"])
