@@ -735,19 +735,25 @@ __device__ __forceinline__ void wave_lds_sync() {
 #endif
 
 // LDS of one scatter wave: a GCHUNK x 64-word mask table (two 32-bit halves per word, so
-// 32-bit LDS atomics) and the compacted list of active (word, bit) entries.
+// 32-bit LDS atomics; the halves adjacent, so a (connection, word) mask is one 64-bit LDS
+// read / write and list entry e = word << 6 | bit addresses its half as u32 index e >> 5) and
+// the compacted list of active (word, bit) entries.
 struct ScatterLds {
-  uint32_t tbl[GCHUNK][2][64];
+  alignas(8) uint32_t tbl[GCHUNK][64][2];
   uint16_t lst[GLIST];
 };
+
+__device__ __forceinline__ uint64_t& tbl_word(ScatterLds& L, int j, int w) {
+  return *reinterpret_cast<uint64_t*>(&L.tbl[j][w][0]);
+}
 
 // Gossip, round r >= 0: every first receipt (v, m) of round r is pushed to k Philox-chosen
 // neighbours.  One wave per (source, GCHUNK-neighbour chunk):
 //   1. the row slice's active bits are compacted into an LDS list (prefix sum of popcounts),
 //      so the 64 lanes evaluate Philox + Floyd for equal shares of messages;
 //   2. picks landing in the chunk set bits of a GCHUNK x 64-word LDS mask table (32-bit LDS
-//      atomics; table = [target][half][word], so the lanes of one batch -- distinct words,
-//      see the rank-major list -- hit distinct banks);
+//      atomics; table = [target][word][half]: one 64-bit LDS access per (target, word) in the
+//      clear and the flush);
 //   3. flush, lane = word: every (target, word) mask leaves as part of one 512 B row access --
 //      STORE_E = false (sparse rounds): row atomicOr into the target's next row + T bit;
 //      STORE_E = true  (dense rounds):  plain store of the whole row (zeros included) into
@@ -786,7 +792,7 @@ __device__ __forceinline__ void scatter_row(const DevGraph& g, const DevState& s
     auto one = [&](uint32_t e, bool ok) {
       const uint32_t wl = e >> 6, bit = e & 63u;
       const uint32_t mg = p.msg_base + (uint32_t)((sl * 64 + (int)wl) * 64) + bit;
-      uint32_t* const col = &L.tbl[0][bit >> 5][wl];
+      uint32_t* const col = &L.tbl[0][0][0] + (e >> 5);  // = &L.tbl[0][wl][bit >> 5]
       const uint32_t mb = ok ? 1u << (bit & 31u) : 0u;
       uint32_t pk[K > 0 ? K : 1];
       gossip_picks_t<(K > 0 ? K : 1)>((uint32_t)p.round, gv, mg, (uint32_t)deg, p.gseed_lo,
@@ -857,14 +863,14 @@ __device__ __forceinline__ void scatter_row(const DevGraph& g, const DevState& s
       for (int j0 = 0; j0 < nn; j0 += gper) {
         const int jj = j0 + gl;
         if (rk && jj < nn) {
-          L.tbl[jj][0][wc] = 0u;
-          L.tbl[jj][1][wc] = 0u;
+          L.tbl[jj][wc][0] = 0u;
+          L.tbl[jj][wc][1] = 0u;
         }
       }
     } else {
       for (int j = 0; j < nn; ++j) {
-        L.tbl[j][0][lane] = 0u;
-        L.tbl[j][1][lane] = 0u;
+        L.tbl[j][lane][0] = 0u;
+        L.tbl[j][lane][1] = 0u;
       }
     }
     // word-major compaction: lane w lists its word's set bits at its exclusive prefix-sum
@@ -896,7 +902,7 @@ __device__ __forceinline__ void scatter_row(const DevGraph& g, const DevState& s
           const uint32_t e = L.lst[i];
           const uint32_t wl = e >> 6, bit = e & 63u;
           const uint32_t mg = p.msg_base + (uint32_t)((sl * 64 + (int)wl) * 64) + bit;
-          uint32_t* const col = &L.tbl[0][bit >> 5][wl];
+          uint32_t* const col = &L.tbl[0][wl][bit >> 5];
           const uint32_t mb = 1u << (bit & 31u);
           uint32_t pk[16];
           gossip_picks((uint32_t)p.round, gv, mg, (uint32_t)deg, k, p.gseed_lo, p.gseed_hi, pk);
@@ -922,7 +928,7 @@ __device__ __forceinline__ void scatter_row(const DevGraph& g, const DevState& s
       const int jj = j0 + gl;
       const bool ok = rk && jj < nn;
       uint64_t x = 0;
-      if (ok) x = all ? fr : (((uint64_t)L.tbl[jj][1][wc] << 32) | L.tbl[jj][0][wc]);
+      if (ok) x = all ? fr : tbl_word(L, jj, wc);
       const uint32_t nj = (uint32_t)__builtin_amdgcn_ds_bpermute(
           (nbr0 + (jj < nn ? jj : 0)) << 2, (int)nbr);
       const uint64_t bal = __ballot(ok && x != 0ull);
@@ -940,7 +946,7 @@ __device__ __forceinline__ void scatter_row(const DevGraph& g, const DevState& s
     return;
   }
   auto tbl_row = [&](int j) -> uint64_t {
-    return ((uint64_t)L.tbl[j][1][lane] << 32) | L.tbl[j][0][lane];
+    return tbl_word(L, j, lane);
   };
   uint64_t xn = use_tbl && nn > 0 ? tbl_row(0) : 0ull;
   for (int j = 0; j < nn; ++j) {
@@ -1315,7 +1321,7 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
         aw |= 1u << a.b;
         if (lane == 0) {
           st.AW[cur][u] = wm;
-          c[ST_ACTIVE_V] += 1;
+          c[ST_ACTIVE_W] += 1u << 16;  // ST_ACTIVE_V, packed (see the fold below)
           c[ST_DEG_ACT] += (uint32_t)deg;
         }
         // this round's pushes, GCHUNK connections at a time.  a.rv holds the receiver slots of
@@ -1357,7 +1363,18 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
       if (sat != sat0) st.S[task] = sat;
     }
 #pragma unroll
-    for (int q = 0; q < STAT_N; ++q) tot[q] += wave_reduce_u32<false>(c[q]);
+    for (int q = 0; q < STAT_N; ++q) {
+      if (q == ST_ACTIVE_V) continue;
+      const uint32_t r = wave_reduce_u32<false>(c[q]);
+      if (q == ST_ACTIVE_W) {
+        // one register for two per-task counts (each <= 64 lanes x 32 peers < 2^16): active
+        // words in the low half, active peers (lane 0) in the high half
+        tot[ST_ACTIVE_W] += r & 0xFFFFu;
+        tot[ST_ACTIVE_V] += r >> 16;
+      } else {
+        tot[q] += r;
+      }
+    }
   }
   PROF_FLUSH
   if (lane == 0) {
