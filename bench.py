@@ -302,6 +302,9 @@ def main():
         "kernel_time_frac_of_step": kernel_ms_total / (elapsed / args.steps * 1e3),
         "relays_per_step_per_gpu": relays / args.steps / world,
         "exchange_ms_per_step": (net.exchange_s * 1e3) if partitioned else 0.0,
+        # compacted exchange: fraction of the boundary rows that had a non-zero word and travelled
+        "exchange_live_row_frac": (net.transport.rows_sent / max(net.transport.rows_total, 1))
+        if partitioned else None,
         "graph_gen_s": t_gen,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

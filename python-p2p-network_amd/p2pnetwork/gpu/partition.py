@@ -91,25 +91,50 @@ class VertexPartition:
         return np.where(held, pos, self.dummy).astype(np.int32)
 
 
+def live_rows(send, send_counts, W):
+    """Compaction of an exchange buffer: (mask, rows, counts) = a uint8 flag per row (row has a
+    non-zero word), the live rows in order, and the live-row count per destination segment.
+    Dead rows carry nothing: a flood row of an inactive boundary peer (the receiver's pull has
+    already cleared the ghost's activity bit for the round) or a gossip ghost nobody pushed to."""
+    import torch
+    n = int(np.sum(send_counts))
+    rows = send[:n * W].view(n, W)
+    live = (rows != 0).any(dim=1)
+    bounds = np.concatenate([[0], np.cumsum(send_counts)]).astype(np.int64)
+    per = [live[int(a):int(b)].sum() for a, b in zip(bounds[:-1], bounds[1:])]
+    counts = torch.stack(per).cpu().numpy().astype(np.int64) if per else np.zeros(0, np.int64)
+    return live.to(torch.uint8), rows[live].reshape(-1), counts
+
+
+def expand_rows(mask, rows, W):
+    """Inverse of live_rows on the receiving side: full rows, zeros where the flag is 0."""
+    import torch
+    full = torch.zeros((mask.numel(), W), dtype=rows.dtype, device=rows.device)
+    full[mask.to(torch.bool)] = rows.view(-1, W)
+    return full.view(-1)
+
+
 class TorchTransport:
     """All-to-all and sum-reduce over a torch.distributed process group.  With the nccl
     backend (RCCL on ROCm) the rows move device-to-device over xGMI; with gloo they are
-    staged through host memory (CPU tests, or two ranks sharing one GPU)."""
+    staged through host memory (CPU tests, or two ranks sharing one GPU).
 
-    def __init__(self, device=None, group=None):
+    Rows go compacted (``sparse``, default): one byte per boundary row says whether the row
+    travels, and only rows with a non-zero word do -- outside the peak rounds most boundary
+    peers are inactive, and the all-to-all moves 512 B per row otherwise."""
+
+    def __init__(self, device=None, group=None, sparse=True):
         import torch
         import torch.distributed as dist
         self.torch, self.dist, self.group = torch, dist, group
         self.backend = dist.get_backend(group)
         self.device = device
+        self.sparse = sparse
+        self.rows_total = 0  # boundary rows offered / actually sent (exchange volume)
+        self.rows_sent = 0
 
-    def alltoall_rows(self, send, send_counts, recv_counts, W):
-        """send: tensor [sum(send_counts) * W] int64 (on self.device); returns the recv tensor."""
+    def _a2a(self, recv, send, outs, ins):
         torch, dist = self.torch, self.dist
-        recv = torch.empty(int(sum(recv_counts)) * W, dtype=torch.int64, device=send.device)
-        ins = [int(c) * W for c in send_counts]
-        outs = [int(c) * W for c in recv_counts]
-        send = send[:sum(ins)]  # exchange buffers are allocated with at least one word
         if self.backend == "nccl":
             dist.all_to_all_single(recv, send, outs, ins, group=self.group)
             torch.cuda.synchronize(send.device)
@@ -117,6 +142,29 @@ class TorchTransport:
         r = recv.cpu()
         dist.all_to_all_single(r, send.cpu(), outs, ins, group=self.group)
         return r.to(send.device)
+
+    def alltoall_rows(self, send, send_counts, recv_counts, W):
+        """send: tensor [sum(send_counts) * W] int64 (on self.device); returns the recv tensor
+        (full rows, in the receiver's list order)."""
+        torch = self.torch
+        n_out, n_in = int(sum(send_counts)), int(sum(recv_counts))
+        self.rows_total += n_out
+        if not self.sparse:
+            self.rows_sent += n_out
+            recv = torch.empty(n_in * W, dtype=torch.int64, device=send.device)
+            return self._a2a(recv, send[:n_out * W], [int(c) * W for c in recv_counts],
+                             [int(c) * W for c in send_counts])
+        mask, rows, live = live_rows(send, send_counts, W)
+        self.rows_sent += int(live.sum())
+        dev = send.device
+        cnt = torch.as_tensor(live, dtype=torch.int64, device=dev)
+        got = self._a2a(torch.empty(len(recv_counts), dtype=torch.int64, device=dev), cnt,
+                        [1] * len(recv_counts), [1] * len(send_counts)).cpu().numpy()
+        rmask = self._a2a(torch.empty(n_in, dtype=torch.uint8, device=dev), mask,
+                          [int(c) for c in recv_counts], [int(c) for c in send_counts])
+        rrows = self._a2a(torch.empty(int(got.sum()) * W, dtype=torch.int64, device=dev), rows,
+                          [int(c) * W for c in got], [int(c) * W for c in live])
+        return expand_rows(rmask, rrows, W)
 
     def allreduce_sum(self, values):
         torch, dist = self.torch, self.dist

@@ -16,8 +16,8 @@ pytestmark = pytest.mark.gpu
 class ThreadTransport:
     """all-to-all / sum-reduce among `world` threads of one process (device tensors)."""
 
-    def __init__(self, shared, rank):
-        self.s, self.rank = shared, rank
+    def __init__(self, shared, rank, sparse=True):
+        self.s, self.rank, self.sparse = shared, rank, sparse
 
     def _gather(self, item):
         s = self.s
@@ -29,7 +29,21 @@ class ThreadTransport:
 
     def alltoall_rows(self, send, send_counts, recv_counts, W):
         import torch
+        from p2pnetwork.gpu.partition import expand_rows, live_rows
         torch.cuda.synchronize()
+        if self.sparse:  # the TorchTransport protocol: row flags + live rows only
+            mask, rows, live = live_rows(send, send_counts, W)
+            items = self._gather((mask, rows, np.asarray(send_counts), live))
+            mp, rp = [], []
+            for m, r, counts, lv in items:
+                off = int(counts[:self.rank].sum())
+                mp.append(m[off:off + int(counts[self.rank])])
+                loff = int(lv[:self.rank].sum()) * W
+                rp.append(r[loff:loff + int(lv[self.rank]) * W])
+            out = expand_rows(torch.cat(mp), torch.cat(rp), W)
+            assert out.numel() == int(np.sum(recv_counts)) * W
+            torch.cuda.synchronize()
+            return out
         items = self._gather((send, np.asarray(send_counts)))
         pieces = []
         for buf, counts in items:
@@ -45,14 +59,14 @@ class ThreadTransport:
         return np.sum(items, axis=0)
 
 
-def run_partitioned(g, world, src, **kw):
+def run_partitioned(g, world, src, sparse=True, **kw):
     from p2pnetwork.gpu import PartitionedNetwork
     shared = {"slots": [None] * world, "barrier": threading.Barrier(world)}
     results, errors = [None] * world, []
 
     def rank_main(rank):
         try:
-            net = PartitionedNetwork(g, world, rank, ThreadTransport(shared, rank), **kw)
+            net = PartitionedNetwork(g, world, rank, ThreadTransport(shared, rank, sparse), **kw)
             with net.net:
                 net.broadcast(src)
                 rounds = net.run()
@@ -89,21 +103,25 @@ def graph(kind):
     return PeerGraph.gnp(5_000, 1.5, seed=2)                   # many small components
 
 
-@pytest.mark.parametrize("kind,mode,M,thr,world", [
-    ("ws", "flood", 64, 0, 2),
-    ("ws", "flood", 130, 400_000_000, 3),
-    ("ba", "flood", 200, 0, 4),
-    ("sparse", "flood", 65, 0, 3),
-    ("ws", "gossip", 64, 0, 2),
-    ("ba", "gossip", 96, 300_000_000, 3),
-    ("sparse", "gossip", 40, 0, 4),
+@pytest.mark.parametrize("kind,mode,M,thr,world,sparse", [
+    ("ws", "flood", 64, 0, 2, True),
+    ("ws", "flood", 64, 0, 2, False),
+    ("ws", "flood", 130, 400_000_000, 3, True),
+    ("ba", "flood", 200, 0, 4, True),
+    ("sparse", "flood", 65, 0, 3, True),
+    ("ws", "gossip", 64, 0, 2, True),
+    ("ws", "gossip", 64, 0, 2, False),
+    ("ba", "gossip", 96, 300_000_000, 3, True),
+    ("sparse", "gossip", 40, 0, 4, True),
 ])
-def test_partitioned_engines_match_single_gpu(kind, mode, M, thr, world):
+def test_partitioned_engines_match_single_gpu(kind, mode, M, thr, world, sparse):
+    """Real engines as threads == one engine == the C oracle; compacted row exchange (only
+    boundary rows with a non-zero word travel) and whole rows."""
     from p2pnetwork.gpu import GraphNetwork, make_sources
     g = graph(kind)
     src = make_sources(g.V, M, seed=21)
     kw = dict(mode=mode, fanout=3, gossip_seed=99, churn_threshold_value=thr, churn_seed=17)
-    res = run_partitioned(g, world, src, record=(mode == "flood"), **kw)
+    res = run_partitioned(g, world, src, sparse=sparse, record=(mode == "flood"), **kw)
     with GraphNetwork(g, record=True, **kw) as one:
         one.broadcast(src)
         rounds1 = one.run()
