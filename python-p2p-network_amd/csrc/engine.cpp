@@ -59,7 +59,8 @@ struct p2pg_engine {
   int32_t* d_recv = nullptr;
   int64_t n_send = 0, n_recv = 0;
   bool last_push_e = false;    // gossip: pushes of the previous round went to E (dense)
-  double e_thresh = 0.1;       // store-mode when active words >= thresh * active rows * W
+  double e_thresh = 0.04;      // store-mode when active words >= thresh * active rows * W
+                               // (c4 A/B, interleaved runs: 0.04 320.4 ms vs 0.1 324.3 ms)
   int push_mode = 0;           // 0 auto, 1 always row atomics, 2 always edge stores
   bool fused = true;           // dense rounds after dense rounds: one pull+scatter pass
   uint64_t prev_aw = 0, prev_av = 0;  // active words / rows of the previous round
@@ -661,6 +662,17 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
     e->last_push_e = use_e;
   }
   if ((rc = read_stats())) return rc;
+#ifdef P2PG_PROF
+  if (fused_round && s.prof && std::getenv("P2PG_PROF_ROUNDS")) {
+    // development builds: per-round fused-kernel segment clocks (then reset)
+    unsigned long long h[9];
+    HIPCHK(e, hipMemcpy(h, s.prof, sizeof(h), hipMemcpyDeviceToHost));
+    HIPCHK(e, hipMemset(s.prof, 0, sizeof(h)));
+    fprintf(stderr, "P2PG_PROF_ROUND %d", e->round);
+    for (int i = 0; i < 9; ++i) fprintf(stderr, " %llu", h[i]);
+    fprintf(stderr, "\n");
+  }
+#endif
   const bool active = tot[ST_NEW] != 0;
   if (out) {
     out->round = e->round;

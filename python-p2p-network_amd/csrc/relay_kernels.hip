@@ -284,6 +284,20 @@ __device__ __forceinline__ uint64_t src_word(const uint64_t* __restrict__ Src, u
   return here ? Src[(int64_t)row * W + pos] : 0ull;
 }
 
+// Packed src_word with the lane set given as a wave-uniform mask: h = the sender's active
+// words (am) & the lanes that still need a word, so the exec mask comes straight from SGPRs
+// (inverse ballot) and the packed position is two mbcnt -- no per-lane bit tests.
+__device__ __forceinline__ uint64_t src_word_m(const uint64_t* __restrict__ Src, uint32_t row,
+                                               int W, uint64_t am, uint64_t h) {
+  uint64_t x = 0ull;
+  if (__builtin_amdgcn_inverse_ballot_w64(h)) {
+    const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(am >> 32),
+                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)am, 0u));
+    x = Src[(int64_t)row * W + pos];
+  }
+  return x;
+}
+
 // Same computation as k_pull for W <= 64 (one row slice), software-pipelined two targets
 // deep so that a target costs ~one memory round trip instead of five: the task's 33 row
 // offsets come in one load; target t+2's seen word and first neighbour chunk are issued, and
@@ -1118,7 +1132,7 @@ constexpr int FG = P2PG_FG;
 // gathers of the next target, which are already in flight.  Hubs (deg > HUB_T) are pulled by k_pull_hub_*
 // and pushed by a chunk-item scatter launch over the hubs only.
 #ifndef P2PG_FUSED_WAVES
-#define P2PG_FUSED_WAVES 1
+#define P2PG_FUSED_WAVES 4  // = 128 VGPRs: 4 waves per SIMD (the gathers spill a few registers per task, not per peer)
 #endif
 template <bool CHURN, int K>
 __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph g, DevState st,
@@ -1195,7 +1209,7 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
     // (of its first 64) still to gather
     uint64_t X[FG];
     auto gather = [&](const PullStage& q, uint64_t& mr) {
-      const uint64_t need = fm & ~q.s;
+      const uint64_t needm = __ballot((fm & ~q.s) != 0ull);
       const int64_t jq = q.beg + lane;
       uint64_t m = __ballot(jq < q.end && ((q.aword >> (q.v & 31)) & 1u));
       // all slot ids / word masks first, then all FG loads back to back: a readlane between
@@ -1216,7 +1230,7 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
         }
       }
 #pragma unroll
-      for (int k = 0; k < FG; ++k) X[k] = src_word(Src, sv[k], W, lane, true, am[k], ok[k] && need);
+      for (int k = 0; k < FG; ++k) X[k] = src_word_m(Src, sv[k], W, am[k], ok[k] ? am[k] & needm : 0ull);
       mr = m;
     };
 
@@ -1243,6 +1257,7 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
       const int64_t u = u0 + a.b;
       const uint64_t deg = (uint64_t)(a.end - a.beg);
       const uint64_t need = fm & ~a.s;
+      const uint64_t needm = __ballot(need != 0ull);
       uint64_t acc = 0;
 #pragma unroll
       for (int k = 0; k < FG; ++k) acc |= X[k];
@@ -1273,7 +1288,7 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
             uint64_t x[8];
 #pragma unroll
             for (int k = 0; k < 8; ++k)
-              x[k] = src_word(Src, sv[k], W, lane, true, am[k], ok[k] && need);
+              x[k] = src_word_m(Src, sv[k], W, am[k], ok[k] ? am[k] & needm : 0ull);
 #pragma unroll
             for (int k = 0; k < 8; ++k) acc |= x[k];
           }
