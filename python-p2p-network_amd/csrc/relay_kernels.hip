@@ -284,6 +284,36 @@ __device__ __forceinline__ uint64_t src_word(const uint64_t* __restrict__ Src, u
   return here ? Src[(int64_t)row * W + pos] : 0ull;
 }
 
+// Per-connection E stores of the gossip dense rounds are non-temporal: the planes are re-read
+// a round later, far beyond L2 / MALL reach, and nt stores retire sooner -- which matters
+// because a wave's next gather wait (vmcnt, in order) also waits for its in-flight stores
+// (c4 A/B: fused rounds 267.9 -> 258.7 ms per step).  P2PG_NT_STORE=0 restores plain stores;
+// P2PG_NT_ROWS / P2PG_NT_LOADS extend nt to the fused kernel's seen / frontier row stores and
+// to its E gathers (development knobs).
+#ifndef P2PG_NT_STORE
+#define P2PG_NT_STORE 1
+#endif
+#ifndef P2PG_NT_ROWS
+#define P2PG_NT_ROWS 0
+#endif
+#ifndef P2PG_NT_LOADS
+#define P2PG_NT_LOADS 0
+#endif
+__device__ __forceinline__ void st_row(uint64_t* p, uint64_t x) {
+#if P2PG_NT_STORE
+  __builtin_nontemporal_store(x, p);
+#else
+  *p = x;
+#endif
+}
+__device__ __forceinline__ void st_frow(uint64_t* p, uint64_t x) {
+#if P2PG_NT_ROWS
+  __builtin_nontemporal_store(x, p);
+#else
+  *p = x;
+#endif
+}
+
 // Packed src_word with the lane set given as a wave-uniform mask: h = the sender's active
 // words (am) & the lanes that still need a word, so the exec mask comes straight from SGPRs
 // (inverse ballot) and the packed position is two mbcnt -- no per-lane bit tests.
@@ -293,7 +323,11 @@ __device__ __forceinline__ uint64_t src_word_m(const uint64_t* __restrict__ Src,
   if (__builtin_amdgcn_inverse_ballot_w64(h)) {
     const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(am >> 32),
                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)am, 0u));
+#if P2PG_NT_LOADS
+    x = __builtin_nontemporal_load(&Src[(int64_t)row * W + pos]);
+#else
     x = Src[(int64_t)row * W + pos];
+#endif
   }
   return x;
 }
@@ -947,7 +981,7 @@ __device__ __forceinline__ void scatter_row(const DevGraph& g, const DevState& s
           (nbr0 + (jj < nn ? jj : 0)) << 2, (int)nbr);
       const uint64_t bal = __ballot(ok && x != 0ull);
       if (STORE_E) {
-        if (ok) Eo[(int64_t)nj * W + rk_lane] = x;
+        if (ok) st_row(&Eo[(int64_t)nj * W + rk_lane], x);
       } else {
         const int64_t u = (int64_t)nj;
         if (x) atomicOr((unsigned long long*)&nx[u * W + sl * 64 + wc], (unsigned long long)x);
@@ -976,9 +1010,9 @@ __device__ __forceinline__ void scatter_row(const DevGraph& g, const DevState& s
       // receiver-major: the row lands in the RECEIVER's slot for this connection, so the
       // pull streams its own contiguous slot range; packed: only the active words, in order
       if (st.AW[cur]) {
-        if (f) Eo[(int64_t)nj * W + __popcll(fam & ((1ull << lane) - 1ull))] = dropped ? 0ull : x;
+        if (f) st_row(&Eo[(int64_t)nj * W + __popcll(fam & ((1ull << lane) - 1ull))], dropped ? 0ull : x);
       } else if (valid) {
-        Eo[(int64_t)nj * W + w] = dropped ? 0ull : x;
+        st_row(&Eo[(int64_t)nj * W + w], dropped ? 0ull : x);
       }
       if (!dropped && lane == 0) c[ST_SCATTER] += (CT)__popcll(bal);
     } else {
@@ -1323,7 +1357,7 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
       const uint64_t nw = acc & need;
       const uint64_t wm = __ballot(nw != 0ull);
       if (nw) {
-        st.seen[u * W + lane] = a.s | nw;
+        st_frow(&st.seen[u * W + lane], a.s | nw);
         const uint32_t pc = (uint32_t)__popcll(nw);
         const uint32_t per_bit = deg < (uint64_t)p.fanout ? (uint32_t)deg : (uint32_t)p.fanout;
         c[ST_NEW] += pc;
@@ -1332,7 +1366,7 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
         c[ST_WEDGES] += (uint32_t)deg;
       }
       if (wm) {
-        if (valid) Fc[u * W + lane] = nw;
+        if (valid) st_frow(&Fc[u * W + lane], nw);
         aw |= 1u << a.b;
         if (lane == 0) {
           st.AW[cur][u] = wm;
