@@ -94,6 +94,47 @@ __device__ __forceinline__ T ldc(const T* p) {
   return *(const __attribute__((address_space(4))) T*)p;
 }
 
+// Per-connection E stores of the gossip dense rounds are non-temporal: the planes are re-read
+// a round later, far beyond L2 / MALL reach, and nt stores retire sooner -- which matters
+// because a wave's next gather wait (vmcnt, in order) also waits for its in-flight stores
+// (c4 A/B: fused rounds 267.9 -> 258.7 ms per step).  P2PG_NT_STORE=0 restores plain stores;
+// P2PG_NT_ROWS / P2PG_NT_LOADS extend nt to the fused kernel's seen / frontier row stores and
+// to its E gathers (development knobs).
+#ifndef P2PG_NT_STORE
+#define P2PG_NT_STORE 1
+#endif
+#ifndef P2PG_NT_ROWS
+#define P2PG_NT_ROWS 0
+#endif
+#ifndef P2PG_NT_LOADS
+#define P2PG_NT_LOADS 0
+#endif
+__device__ __forceinline__ void st_row(uint64_t* p, uint64_t x) {
+#if P2PG_NT_STORE
+  __builtin_nontemporal_store(x, p);
+#else
+  *p = x;
+#endif
+}
+#ifndef P2PG_NT_PULL
+#define P2PG_NT_PULL 1  // c4 update kernel 13.3 -> 12.7 ms per step; c3 flood pull unchanged
+#endif
+// seen / frontier / push-row stores of the pull and update kernels, non-temporal too
+__device__ __forceinline__ void st_prow(uint64_t* p, uint64_t x) {
+#if P2PG_NT_PULL
+  __builtin_nontemporal_store(x, p);
+#else
+  *p = x;
+#endif
+}
+__device__ __forceinline__ void st_frow(uint64_t* p, uint64_t x) {
+#if P2PG_NT_ROWS
+  __builtin_nontemporal_store(x, p);
+#else
+  *p = x;
+#endif
+}
+
 // Global peer id of a local vertex (partitioned runs keep ghosts in global-id order; the
 // Philox keys of churn and gossip are global ids so partitioning cannot change results).
 __device__ __forceinline__ uint32_t gidx(const DevGraph& g, int64_t x) {
@@ -223,10 +264,10 @@ __global__ __launch_bounds__(256) void k_pull(DevGraph g, DevState st, RoundPara
         const bool any = __ballot(nw != 0ull) != 0ull;
         row_new |= any;
         if (__ballot(valid && (s | nw) != fm)) row_full = false;
-        if (nw) st.seen[u * W + w] = s | nw;
+        if (nw) st_prow(&st.seen[u * W + w], s | nw);
         // single-slice rows are written only when active; multi-slice rows always (a row
         // must be whole whenever its A bit is set)
-        if (valid && (any || nslices > 1)) Fc[u * W + w] = nw;
+        if (valid && (any || nslices > 1)) st_prow(&Fc[u * W + w], nw);
         if (nw) {
           const uint64_t pc = (uint64_t)__popcll(nw);
           c[ST_NEW] += pc;
@@ -284,35 +325,6 @@ __device__ __forceinline__ uint64_t src_word(const uint64_t* __restrict__ Src, u
   return here ? Src[(int64_t)row * W + pos] : 0ull;
 }
 
-// Per-connection E stores of the gossip dense rounds are non-temporal: the planes are re-read
-// a round later, far beyond L2 / MALL reach, and nt stores retire sooner -- which matters
-// because a wave's next gather wait (vmcnt, in order) also waits for its in-flight stores
-// (c4 A/B: fused rounds 267.9 -> 258.7 ms per step).  P2PG_NT_STORE=0 restores plain stores;
-// P2PG_NT_ROWS / P2PG_NT_LOADS extend nt to the fused kernel's seen / frontier row stores and
-// to its E gathers (development knobs).
-#ifndef P2PG_NT_STORE
-#define P2PG_NT_STORE 1
-#endif
-#ifndef P2PG_NT_ROWS
-#define P2PG_NT_ROWS 0
-#endif
-#ifndef P2PG_NT_LOADS
-#define P2PG_NT_LOADS 0
-#endif
-__device__ __forceinline__ void st_row(uint64_t* p, uint64_t x) {
-#if P2PG_NT_STORE
-  __builtin_nontemporal_store(x, p);
-#else
-  *p = x;
-#endif
-}
-__device__ __forceinline__ void st_frow(uint64_t* p, uint64_t x) {
-#if P2PG_NT_ROWS
-  __builtin_nontemporal_store(x, p);
-#else
-  *p = x;
-#endif
-}
 
 // Packed src_word with the lane set given as a wave-uniform mask: h = the sender's active
 // words (am) & the lanes that still need a word, so the exec mask comes straight from SGPRs
@@ -481,7 +493,7 @@ __global__ __launch_bounds__(256, P2PG_PULL_WAVES) void k_pull1(DevGraph g, DevS
       const uint64_t nw = acc & need;
       const bool any = __ballot(nw != 0ull) != 0ull;
       if (nw) {
-        st.seen[u * W + lane] = s1.s | nw;
+        st_prow(&st.seen[u * W + lane], s1.s | nw);
         const uint64_t pc = (uint64_t)__popcll(nw);
         const uint64_t per_bit = GOSSIP ? (deg < (uint64_t)p.fanout ? deg : (uint64_t)p.fanout)
                                         : deg - 1;
@@ -491,7 +503,7 @@ __global__ __launch_bounds__(256, P2PG_PULL_WAVES) void k_pull1(DevGraph g, DevS
         c[ST_WEDGES] += deg;
       }
       if (any) {
-        if (valid) Fc[u * W + lane] = nw;
+        if (valid) st_prow(&Fc[u * W + lane], nw);
         aw |= 1u << s1.b;
         const uint64_t wm = __ballot(nw != 0ull);
         if (lane == 0) {
@@ -606,7 +618,7 @@ __global__ __launch_bounds__(256) void k_pull_hub_finalize(DevGraph g, DevState 
     const uint64_t nw = acc & fm & ~s;
     const uint64_t deg = (uint64_t)(g.rowptr[u + 1] - g.rowptr[u]);
     if (nw) {
-      st.seen[u * W + lane] = s | nw;
+      st_prow(&st.seen[u * W + lane], s | nw);
       const uint64_t pc = (uint64_t)__popcll(nw);
       const uint64_t per_bit = GOSSIP ? (deg < (uint64_t)p.fanout ? deg : (uint64_t)p.fanout)
                                       : deg - 1;
@@ -616,7 +628,7 @@ __global__ __launch_bounds__(256) void k_pull_hub_finalize(DevGraph g, DevState 
       c[ST_WEDGES] += deg;
     }
     if (__ballot(nw != 0ull)) {
-      if (valid) st.F[cur][u * W + lane] = nw;
+      if (valid) st_prow(&st.F[cur][u * W + lane], nw);
       const uint64_t wm = __ballot(nw != 0ull);
       if (lane == 0) {
         if (GOSSIP && st.AW[cur]) st.AW[cur][u] = wm;
@@ -669,7 +681,7 @@ __global__ __launch_bounds__(256) void k_gossip_update(DevGraph g, DevState st,
         if (valid) {
           x = nx[u * W + w];
           if (x) {
-            nx[u * W + w] = 0ull;
+            st_prow(&nx[u * W + w], 0ull);
             s = st.seen[u * W + w];
             c[ST_AUX] += 1;  // touched (pushed-to) words consumed
           }
@@ -679,8 +691,8 @@ __global__ __launch_bounds__(256) void k_gossip_update(DevGraph g, DevState st,
         const bool any = wm != 0ull;
         row_new |= any;
         if (any && nslices == 1 && st.AW[cur] && lane == 0) st.AW[cur][u] = wm;
-        if (nw) st.seen[u * W + w] = s | nw;
-        if (valid && (any || nslices > 1)) Fc[u * W + w] = nw;
+        if (nw) st_prow(&st.seen[u * W + w], s | nw);
+        if (valid && (any || nslices > 1)) st_prow(&Fc[u * W + w], nw);
         if (nw) {
           const uint64_t pc = (uint64_t)__popcll(nw);
           c[ST_NEW] += pc;
