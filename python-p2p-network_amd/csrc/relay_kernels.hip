@@ -97,17 +97,18 @@ __device__ __forceinline__ T ldc(const T* p) {
 // Per-connection E stores of the gossip dense rounds are non-temporal: the planes are re-read
 // a round later, far beyond L2 / MALL reach, and nt stores retire sooner -- which matters
 // because a wave's next gather wait (vmcnt, in order) also waits for its in-flight stores
-// (c4 A/B: fused rounds 267.9 -> 258.7 ms per step).  P2PG_NT_STORE=0 restores plain stores;
+// (c4 A/B: fused rounds 267.9 -> 258.7 ms per step).  P2PG_NT_STORE=0 restores plain stores.
 // P2PG_NT_ROWS / P2PG_NT_LOADS extend nt to the fused kernel's seen / frontier row stores and
-// to its E gathers (development knobs).
+// to its E gathers (read once per receiver): together another 260.6 -> 258.7 ms (3 interleaved
+// pairs).
 #ifndef P2PG_NT_STORE
 #define P2PG_NT_STORE 1
 #endif
 #ifndef P2PG_NT_ROWS
-#define P2PG_NT_ROWS 0
+#define P2PG_NT_ROWS 1
 #endif
 #ifndef P2PG_NT_LOADS
-#define P2PG_NT_LOADS 0
+#define P2PG_NT_LOADS 1
 #endif
 __device__ __forceinline__ void st_row(uint64_t* p, uint64_t x) {
 #if P2PG_NT_STORE
