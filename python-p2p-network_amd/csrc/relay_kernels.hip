@@ -110,6 +110,19 @@ __device__ __forceinline__ T ldc(const T* p) {
 #ifndef P2PG_NT_LOADS
 #define P2PG_NT_LOADS 1
 #endif
+#ifndef P2PG_NT_ISSUE
+#define P2PG_NT_ISSUE 0
+#endif
+// streamed-once loads of the fused kernel's row stage (seen word, neighbour ids, receiver slots);
+// nt here measured ±0 (3 interleaved c4 pairs), so off by default
+template <class T>
+__device__ __forceinline__ T ld_once(const T* p) {
+#if P2PG_NT_ISSUE
+  return __builtin_nontemporal_load(p);
+#else
+  return *p;
+#endif
+}
 __device__ __forceinline__ void st_row(uint64_t* p, uint64_t x) {
 #if P2PG_NT_STORE
   __builtin_nontemporal_store(x, p);
@@ -1226,12 +1239,12 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
       if (b < 0) return;
       q.beg = readlane64(rp, b);
       q.end = readlane64(rp, b + 1);
-      if (valid) q.s = st.seen[(u0 + b) * W + lane];
+      if (valid) q.s = ld_once(&st.seen[(u0 + b) * W + lane]);
       const int64_t j = q.beg + lane;
       if (j < q.end) {
-        q.v = g.colidx[j];
+        q.v = ld_once(&g.colidx[j]);
         q.r = (uint32_t)j;
-        q.rv = g.rev[j];
+        q.rv = ld_once(&g.rev[j]);
       }
     };
     // loads only; gather() tests the bit (see k_pull1)
