@@ -838,7 +838,9 @@ __device__ __forceinline__ uint64_t& tbl_word(ScatterLds& L, int j, int w) {
 // (row atomics).  Every
 // per-source value is a scalar load or a lane of a prefetched register: a vector load here
 // would make the wave wait (vmcnt) for its own in-flight row stores / atomics.
-template <bool CHURN, int K, bool STORE_E, class CT>
+// PH: 0 = the whole push; 1 = table + picks only (the flush follows later, PH 2, with the same
+// source, f and receiver slots: the fused kernel defers a short row's flush by one target).
+template <bool CHURN, int K, bool STORE_E, int PH = 0, class CT>
 __device__ __forceinline__ void scatter_row(const DevGraph& g, const DevState& st,
                                             const RoundParams& p, ScatterLds& L, int lane,
                                             int64_t v, int64_t rb, int64_t deg, int chunk,
@@ -932,7 +934,7 @@ __device__ __forceinline__ void scatter_row(const DevGraph& g, const DevState& s
   }
   const int gper = 64 / seg;
 
-  if (use_tbl) {
+  if (PH != 2 && use_tbl) {
     if (compact) {
       for (int j0 = 0; j0 < nn; j0 += gper) {
         const int jj = j0 + gl;
@@ -990,6 +992,7 @@ __device__ __forceinline__ void scatter_row(const DevGraph& g, const DevState& s
       PROF_MARK(7);
     }
   }
+  if constexpr (PH == 1) return;
   if (compact) {
     const uint64_t segm = (1ull << seg) - 1ull;
     uint64_t fr = 0;
@@ -1303,6 +1306,21 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
     uint32_t c[STAT_N] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t aw = 0, sat = sat0;
     uint32_t rest = todo;
+    // The flush (E stores) of a short row (deg <= GCHUNK) is deferred to the next target,
+    // after that target's gather wait: a wait issued right behind a row's stores would also
+    // wait for their completion (vmcnt counts loads and stores in order); one target later,
+    // the picks in between have covered it.
+    bool pend = false;
+    int64_t pu = 0, pbeg = 0, pdeg = 0;
+    uint64_t pnw = 0;
+    uint32_t prv = 0;
+    auto flush_pending = [&]() {
+      if (pend) {
+        scatter_row<CHURN, K, true, 2>(g, st, p, lds[wib], lane, pu, pbeg, pdeg, 0, 0, pnw, prv,
+                                       0, c PROF_PASS);
+        pend = false;
+      }
+    };
     PullStage sA, sB, sC, sD;
     issue(sA, next_bit(rest));
     issue(sB, next_bit(rest));
@@ -1374,6 +1392,7 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
       // until those gathers return).
       __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
       PROF_MARK(1);
+      flush_pending();
       // advance the pipeline before this target's stores and picks: gathers of t+1 (their
       // activity words were loaded a target ago), activity words of t+2, rows of t+3
       if (b.b >= 0) gather(b, b.mr);
@@ -1404,7 +1423,16 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
         // every 4 chunks and wait for them right there -- a load that MAY be in flight when
         // the picks read the slots would make the compiler wait for everything, the next
         // target's gathers included.
-        if (deg <= 64) {
+        if (deg <= (uint64_t)GCHUNK) {
+          scatter_row<CHURN, K, true, 1>(g, st, p, lds[wib], lane, u, a.beg, (int64_t)deg, 0, 0,
+                                         nw, a.rv, 0, c PROF_PASS);
+          pend = true;
+          pu = u;
+          pbeg = a.beg;
+          pdeg = (int64_t)deg;
+          pnw = nw;
+          prv = a.rv;
+        } else if (deg <= 64) {
           for (int ch = 0; (int64_t)ch * GCHUNK < (int64_t)deg; ++ch)
             scatter_row<CHURN, K, true>(g, st, p, lds[wib], lane, u, a.beg, (int64_t)deg, ch, 0,
                                         nw, a.rv, ch * GCHUNK, c PROF_PASS);
@@ -1432,6 +1460,7 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
       if (sD.b < 0) break;
       step(sD, sA, sB, sC);
     }
+    flush_pending();
     PROF_MARK(4);
     if (lane == 0) {
       st.A[cur][task] = aw;
