@@ -107,6 +107,14 @@ void p2pg_graph_free(p2pg_graph* g);
 int p2pg_make_sources(int64_t V, int32_t M, uint64_t seed, uint32_t msg_id_base, int32_t* src);
 /* Host Philox4x32-10 (KAT hook). */
 void p2pg_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
+/* Host evaluation of the engine's random draws (the wire bridge replays the sends of a run):
+ * the connections (indices into the peer's ascending adjacency) a gossip first receipt of
+ * message msg (global id) at peer in round `round` is pushed to, in draw order -- what
+ * Node.send_to_node is called on (node.py:114-120); returns their number min(k, deg).     */
+int p2pg_gossip_targets(uint32_t round, uint32_t peer, uint32_t msg, uint32_t deg, int32_t k,
+                        uint64_t seed, uint32_t* out);
+/* 1 iff a send over {a, b} made in round `round` is lost to churn.       */
+int p2pg_churn_lost(uint32_t round, uint32_t a, uint32_t b, uint32_t threshold, uint64_t seed);
 
 /* ---- engine ------------------------------------------------------------------------- */
 int p2pg_create(const p2pg_config* cfg, p2pg_engine** out);
@@ -126,6 +134,9 @@ int p2pg_get_new_deliveries(p2pg_engine* e, int64_t cap, int32_t* peer, int32_t*
 /* Validation copies: seen [V][W] uint64 (W = ceil(M/64)); hop/parent [V][M] int32 need
  * P2PG_FLAG_RECORD (-1 = not delivered).  Any pointer may be NULL.                      */
 int p2pg_read_planes(p2pg_engine* e, uint64_t* seen, int32_t* hop, int32_t* parent);
+/* Word w of every peer's seen row (messages 64w .. 64w+63): out[V].  Full-size validation
+ * without copying a whole plane (config 5: 51 GB at 100M peers x 4096 broadcasts).       */
+int p2pg_read_seen_word(p2pg_engine* e, int32_t w, uint64_t* out);
 /* Summed device time per kernel class since the last reset (needs P2PG_FLAG_TIMING):
  * 0 seed (origination), 1 flood pull, 2 gossip scatter by row atomics (sparse rounds),
  * 3 record (validation), 4 gossip update (consume row atomics), 5 gossip pull (consume edge

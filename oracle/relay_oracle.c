@@ -15,6 +15,7 @@
  * frontier row rewritten each round, no activity bitmaps), atomic-OR pushes for gossip.
  * Pinned by tests/test_oracle_golden.py against the reference-harness fixtures.
  *
+ * seen_out (optional, [V][W] uint64): every peer's seen set at quiescence.
  * stats[r*8 + i]: 0 new deliveries, 1 relays, 2 active peers, 3 active words, 4 wedges,
  * 5 deg of active peers, 6 gossip scatter words, 7 unused.
  */
@@ -97,7 +98,7 @@ static void round0(int64_t V, const int64_t* rp, int32_t M, const int32_t* src, 
 
 int oracle_flood(int64_t V, const int64_t* rp, const int32_t* ci, int32_t M, const int32_t* src,
                  uint32_t churn_thr, uint64_t churn_seed, int32_t max_rounds, uint64_t* stats,
-                 int32_t* n_rounds, int32_t* hop, int32_t* par) {
+                 int32_t* n_rounds, int32_t* hop, int32_t* par, uint64_t* seen_out) {
   const int64_t W = (M + 63) / 64;
   uint64_t* seen = calloc((size_t)(V * W), 8);
   uint64_t* F = calloc((size_t)(V * W), 8);
@@ -107,6 +108,7 @@ int oracle_flood(int64_t V, const int64_t* rp, const int32_t* ci, int32_t M, con
     return -4;
   }
   if (hop) {
+#pragma omp parallel for schedule(static)
     for (int64_t i = 0; i < V * M; ++i) hop[i] = par[i] = -1;
   }
   memset(stats, 0, sizeof(uint64_t) * 8 * (size_t)max_rounds);
@@ -123,6 +125,9 @@ int oracle_flood(int64_t V, const int64_t* rp, const int32_t* ci, int32_t M, con
         memset(acc, 0, sizeof(uint64_t) * W);
         for (int64_t e = rp[u]; e < rp[u + 1]; ++e) {
           const int64_t v = ci[e];
+          uint64_t any_v = 0; /* nothing sent by v: no churn draw needed */
+          for (int64_t w = 0; w < W; ++w) any_v |= F[v * W + w];
+          if (!any_v) continue;
           if (dropped((uint32_t)(r - 1), (uint32_t)u, (uint32_t)v, churn_thr, churn_seed)) continue;
           for (int64_t w = 0; w < W; ++w) acc[w] |= F[v * W + w];
         }
@@ -142,6 +147,7 @@ int oracle_flood(int64_t V, const int64_t* rp, const int32_t* ci, int32_t M, con
             uint64_t pend = nw;
             for (int64_t e = rp[u]; e < rp[u + 1] && pend; ++e) {
               const int64_t v = ci[e];
+              if (!(F[v * W + w] & pend)) continue;
               if (dropped((uint32_t)(r - 1), (uint32_t)u, (uint32_t)v, churn_thr, churn_seed)) continue;
               uint64_t hit = F[v * W + w] & pend;
               pend &= ~hit;
@@ -172,6 +178,7 @@ int oracle_flood(int64_t V, const int64_t* rp, const int32_t* ci, int32_t M, con
     }
   }
   *n_rounds = r;
+  if (seen_out) memcpy(seen_out, seen, sizeof(uint64_t) * (size_t)(V * W));
   free(seen), free(F), free(Fn);
   return 0;
 }
@@ -184,7 +191,7 @@ static int cmp_u64(const void* a, const void* b) {
 int oracle_gossip(int64_t V, const int64_t* rp, const int32_t* ci, int32_t M,
                   const int32_t* src, int32_t k, uint64_t gseed, uint32_t msg_base,
                   uint32_t churn_thr, uint64_t churn_seed, int32_t max_rounds, uint64_t* stats,
-                  int32_t* n_rounds, int32_t* hop, int32_t* par) {
+                  int32_t* n_rounds, int32_t* hop, int32_t* par, uint64_t* seen_out) {
   const int64_t W = (M + 63) / 64;
   uint64_t* seen = calloc((size_t)(V * W), 8);
   uint64_t* F = calloc((size_t)(V * W), 8);
@@ -195,6 +202,7 @@ int oracle_gossip(int64_t V, const int64_t* rp, const int32_t* ci, int32_t M,
     return -4;
   }
   if (hop) {
+#pragma omp parallel for schedule(static)
     for (int64_t i = 0; i < V * M; ++i) hop[i] = par[i] = -1, cand[i] = 0x7FFFFFFF;
   }
   memset(stats, 0, sizeof(uint64_t) * 8 * (size_t)max_rounds);
@@ -288,6 +296,7 @@ int oracle_gossip(int64_t V, const int64_t* rp, const int32_t* ci, int32_t M,
     st[0] = s0, st[1] = s1, st[2] = s2, st[3] = s3, st[4] = s4, st[5] = s5;
   }
   *n_rounds = r;
+  if (seen_out) memcpy(seen_out, seen, sizeof(uint64_t) * (size_t)(V * W));
   free(seen), free(F), free(nx), free(cand);
   return 0;
 }

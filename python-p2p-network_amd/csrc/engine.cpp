@@ -784,6 +784,21 @@ int p2pg_read_planes(p2pg_engine* e, uint64_t* seen, int32_t* hop, int32_t* pare
   return P2PG_OK;
 }
 
+int p2pg_read_seen_word(p2pg_engine* e, int32_t w, uint64_t* out) {
+  if (!e || !e->have_state) return fail(e, P2PG_ERR_STATE, "read_seen_word: no state");
+  if (w < 0 || w >= e->W || !out) return fail(e, P2PG_ERR_ARG, "read_seen_word: word out of range");
+  HIPCHK(e, hipSetDevice(e->cfg.device));
+  // column w of the [V][W] plane gathered into a contiguous device buffer, then one copy
+  uint64_t* col = nullptr;
+  HIPCHK(e, hipMalloc((void**)&col, sizeof(uint64_t) * (size_t)e->V));
+  hipError_t r = launch_column(e->st.seen, e->W, w, e->V, col, e->stream);
+  if (r == hipSuccess) r = hipStreamSynchronize(e->stream);
+  if (r == hipSuccess) r = hipMemcpy(out, col, sizeof(uint64_t) * (size_t)e->V, hipMemcpyDeviceToHost);
+  (void)hipFree(col);
+  if (r != hipSuccess) return fail(e, P2PG_ERR_HIP, std::string("read_seen_word: ") + hipGetErrorString(r));
+  return P2PG_OK;
+}
+
 int p2pg_set_global_ids(p2pg_engine* e, const int32_t* gid) {
   if (!e || !e->d_rowptr) return fail(e, P2PG_ERR_STATE, "set_global_ids: load a graph first");
   HIPCHK(e, hipSetDevice(e->cfg.device));
@@ -1001,17 +1016,21 @@ uint64_t graph_hash(const p2pg_engine* e) {
   return fnv1a(h, e->h_colidx.data(), e->h_colidx.size() * sizeof(int32_t));
 }
 
-int64_t snapshot_bytes(const p2pg_engine* e) {
+int64_t snapshot_bytes(const p2pg_engine* e, bool with_next, bool with_record) {
   int64_t n = (int64_t)sizeof(SnapHeader) + 2 * (int64_t)e->plane_bytes + 2 * (int64_t)e->bm_bytes;
-  if (e->st.next[0]) n += (int64_t)e->plane_bytes + (int64_t)e->bm_bytes;
-  if (e->st.hop) n += 2 * (int64_t)e->V * e->M * (int64_t)sizeof(int32_t);
+  if (with_next) n += (int64_t)e->plane_bytes + (int64_t)e->bm_bytes;
+  if (with_record) n += 2 * (int64_t)e->V * e->M * (int64_t)sizeof(int32_t);
   return n;
+}
+
+int64_t snapshot_bytes(const p2pg_engine* e) {
+  return snapshot_bytes(e, e->st.next[0] != nullptr, e->st.hop != nullptr);
 }
 
 // The planes of a snapshot, in order: seen, saturated bits, the last round's activity bits and
 // frontier (its first receipts), [pending row pushes + their bits], [hop, parent].
 template <class F>
-int for_planes(p2pg_engine* e, F&& f) {
+int for_planes(p2pg_engine* e, bool with_next, F&& f) {
   DevState& s = e->st;
   const int last = (e->round + 1) & 1;  // (round - 1) & 1
   const int nx = e->round & 1;
@@ -1020,7 +1039,7 @@ int for_planes(p2pg_engine* e, F&& f) {
   if ((rc = f((void*)s.S, e->bm_bytes))) return rc;
   if ((rc = f((void*)s.A[last], e->bm_bytes))) return rc;
   if ((rc = f((void*)s.F[last], e->plane_bytes))) return rc;
-  if (s.next[0]) {
+  if (with_next) {
     if ((rc = f((void*)s.next[nx], e->plane_bytes))) return rc;
     if ((rc = f((void*)s.T[nx], e->bm_bytes))) return rc;
   }
@@ -1086,7 +1105,7 @@ int p2pg_snapshot(p2pg_engine* e, void* buf, int64_t cap) {
   char* out = (char*)buf;
   std::memcpy(out, &h, sizeof(h));
   size_t off = sizeof(h);
-  return for_planes(e, [&](void* dev, size_t n) -> int {
+  return for_planes(e, s.next[0] != nullptr, [&](void* dev, size_t n) -> int {
     if (n) HIPCHK(e, hipMemcpy(out + off, dev, n, hipMemcpyDeviceToHost));
     off += n;
     return P2PG_OK;
@@ -1109,17 +1128,24 @@ int p2pg_restore(p2pg_engine* e, const void* buf, int64_t size) {
     return fail(e, P2PG_ERR_STATE, "restore: graph differs from the snapshot's");
   if (h.M != e->M || h.src_hash != fnv1a(0xCBF29CE484222325ull, e->h_src.data(), e->h_src.size() * sizeof(int32_t)))
     return fail(e, P2PG_ERR_STATE, "restore: broadcast sources differ from the snapshot's");
+  // validate everything before the engine is touched: a rejected snapshot leaves it as it was
+  if (h.round < 0 || h.has_next > 1 || h.done > 1 || h.consume_next > 1 ||
+      (h.consume_next && !h.has_next))
+    return fail(e, P2PG_ERR_ARG, "restore: corrupt snapshot header");
+  const bool with_next = h.has_next != 0;
+  if (size < snapshot_bytes(e, with_next, (h.flags & P2PG_FLAG_RECORD) != 0))
+    return fail(e, P2PG_ERR_ARG, "restore: snapshot truncated");
   HIPCHK(e, hipSetDevice(e->cfg.device));
-  int rc = p2pg_reset(e);
-  if (rc) return rc;
   DevState& s = e->st;
-  if (h.has_next && !s.next[0]) {  // flood run that had a topology update
+  if (with_next && !s.next[0]) {  // flood run that had a topology update
     for (int i = 0; i < 2; ++i) {
       HIPCHK(e, hipMalloc((void**)&s.next[i], e->plane_bytes ? e->plane_bytes : 8));
       HIPCHK(e, hipMalloc((void**)&s.T[i], e->bm_bytes ? e->bm_bytes : 8));
     }
   }
-  if (s.next[0]) {
+  int rc = p2pg_reset(e);
+  if (rc) return rc;
+  if (s.next[0]) {  // pending pushes: from the snapshot, or none (a flood snapshot without them)
     for (int i = 0; i < 2; ++i) {
       HIPCHK(e, hipMemsetAsync(s.next[i], 0, e->plane_bytes, e->stream));
       HIPCHK(e, hipMemsetAsync(s.T[i], 0, e->bm_bytes, e->stream));
@@ -1133,11 +1159,9 @@ int p2pg_restore(p2pg_engine* e, const void* buf, int64_t size) {
   e->total_relays = h.total_relays;
   e->prev_aw = h.prev_aw;
   e->prev_av = h.prev_av;
-  if (size < snapshot_bytes(e) || (h.has_next != 0) != (s.next[0] != nullptr))
-    return fail(e, P2PG_ERR_ARG, "restore: snapshot truncated or of another layout");
   const char* in = (const char*)buf;
   size_t off = sizeof(h);
-  rc = for_planes(e, [&](void* dev, size_t n) -> int {
+  rc = for_planes(e, with_next, [&](void* dev, size_t n) -> int {
     if (n) HIPCHK(e, hipMemcpy(dev, in + off, n, hipMemcpyHostToDevice));
     off += n;
     return P2PG_OK;

@@ -363,6 +363,24 @@ void p2pg_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t o
   out[3] = r.w;
 }
 
+int p2pg_gossip_targets(uint32_t round, uint32_t peer, uint32_t msg, uint32_t deg, int32_t k,
+                        uint64_t seed, uint32_t* out) {
+  if (k < 1 || k > 16 || (deg > 0 && !out)) {
+    set_global_error("gossip_targets: need 1 <= k <= 16 and an output array");
+    return P2PG_ERR_ARG;
+  }
+  if (deg <= (uint32_t)k) {  // every connection, in adjacency order
+    for (uint32_t j = 0; j < deg; ++j) out[j] = j;
+    return (int)deg;
+  }
+  gossip_picks(round, peer, msg, deg, k, (uint32_t)seed, (uint32_t)(seed >> 32), out);
+  return k;
+}
+
+int p2pg_churn_lost(uint32_t round, uint32_t a, uint32_t b, uint32_t threshold, uint64_t seed) {
+  return churn_dropped(round, a, b, threshold, (uint32_t)seed, (uint32_t)(seed >> 32)) ? 1 : 0;
+}
+
 const char* p2pg_global_error(void) { return g_error.c_str(); }
 
 }  // extern "C"

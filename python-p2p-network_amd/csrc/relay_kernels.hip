@@ -1643,6 +1643,13 @@ __global__ __launch_bounds__(256) void k_unpack(DevState st, int plane, int roun
   }
 }
 
+__global__ void k_column(const uint64_t* __restrict__ plane, int32_t W, int32_t w, int64_t V,
+                         uint64_t* __restrict__ out) {
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < V;
+       v += (int64_t)gridDim.x * blockDim.x)
+    out[v] = plane[v * W + w];
+}
+
 __global__ void k_philox(int32_t n, const uint32_t* ctr, uint32_t k0, uint32_t k1,
                          uint32_t* out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1876,6 +1883,14 @@ hipError_t launch_unpack(const DevState& st, int plane, int round, const int32_t
                          const uint64_t* in, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_unpack, dim3(grid_tasks(n)), dim3(256), 0, s, st, plane, round, ids, n, in);
+  return hipGetLastError();
+}
+
+hipError_t launch_column(const uint64_t* plane, int32_t W, int32_t w, int64_t V, uint64_t* out,
+                         hipStream_t s) {
+  if (V <= 0) return hipSuccess;
+  const int64_t blocks = std::min<int64_t>((V + 255) / 256, 8192);
+  hipLaunchKernelGGL(k_column, dim3((unsigned)blocks), dim3(256), 0, s, plane, W, w, V, out);
   return hipGetLastError();
 }
 

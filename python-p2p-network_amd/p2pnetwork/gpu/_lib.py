@@ -79,6 +79,8 @@ SIGNATURES = {
     "p2pg_graph_free": (None, [_P]),
     "p2pg_make_sources": (ctypes.c_int, [_I64, _I32, _U64, _U32, _P]),
     "p2pg_philox4x32_10": (None, [_P, _P, _P]),
+    "p2pg_gossip_targets": (ctypes.c_int, [_U32, _U32, _U32, _U32, _I32, _U64, _P]),
+    "p2pg_churn_lost": (ctypes.c_int, [_U32, _U32, _U32, _U32, _U64]),
     "p2pg_create": (ctypes.c_int, [ctypes.POINTER(Config), _PP]),
     "p2pg_load_csr": (ctypes.c_int, [_P, _I64, _P, _P]),
     "p2pg_set_sources": (ctypes.c_int, [_P, _I32, _P]),
@@ -87,6 +89,7 @@ SIGNATURES = {
     "p2pg_run": (ctypes.c_int, [_P, _I32, _P, ctypes.POINTER(_I32)]),
     "p2pg_get_new_deliveries": (ctypes.c_int, [_P, _I64, _P, _P, _P, _P, ctypes.POINTER(_I64)]),
     "p2pg_read_planes": (ctypes.c_int, [_P, _P, _P, _P]),
+    "p2pg_read_seen_word": (ctypes.c_int, [_P, _I32, _P]),
     "p2pg_kernel_times": (ctypes.c_int, [_P, _P, _P]),
     "p2pg_set_global_ids": (ctypes.c_int, [_P, _P]),
     "p2pg_set_exchange": (ctypes.c_int, [_P, _I64, _P, _I64, _P]),

@@ -275,6 +275,13 @@ class GraphNetwork:
         self._check(_lib.lib().p2pg_read_planes(self._h, _lib.ptr(out), None, None))
         return out
 
+    def seen_word(self, w):
+        """uint64 [V]: word w of every peer's seen row (messages 64w .. 64w+63), without
+        copying the whole plane (p2pg_read_seen_word)."""
+        out = np.zeros(self.graph.V, dtype=np.uint64)
+        self._check(_lib.lib().p2pg_read_seen_word(self._h, int(w), _lib.ptr(out)))
+        return out
+
     def delivered(self):
         """bool [V, M]: peer v has received broadcast m (its dedup 'seen' set)."""
         s = self.seen_plane()

@@ -224,6 +224,15 @@ class PartitionedNetwork:
                           wedges=int(deg[words // W].sum()), deg_active=int(deg[vs].sum()),
                           scatter_words=0, touched_words=0)
 
+    @staticmethod
+    def _ready(t):
+        """The transport builds the received rows with torch ops on torch's current stream; the
+        engine unpacks on its own stream, so wait for them first (nothing else orders them)."""
+        if getattr(t, "is_cuda", False):
+            import torch
+            torch.cuda.current_stream(t.device).synchronize()
+        return t
+
     def _exchange(self):
         if self.world == 1:
             return
@@ -233,12 +242,12 @@ class PartitionedNetwork:
             send = self.net.alloc_exchange(int(p.send_counts.sum()) * W)
             self.net.exchange_pack(0, send)
             recv = self.transport.alltoall_rows(send, p.send_counts, p.recv_counts, W)
-            self.net.exchange_unpack(0, recv)
+            self.net.exchange_unpack(0, self._ready(recv))
         else:                      # gossip pushes: ghost holder -> owner
             send = self.net.alloc_exchange(int(p.recv_counts.sum()) * W)
             self.net.exchange_pack(1, send)
             recv = self.transport.alltoall_rows(send, p.recv_counts, p.send_counts, W)
-            self.net.exchange_unpack(1, recv)
+            self.net.exchange_unpack(1, self._ready(recv))
 
     def step(self):
         st = self.net.step()

@@ -17,10 +17,42 @@ def pytest_configure(config):
 
 
 def golden_cases(prefix="", dynamic=False):
-    """Golden fixture names; dynamic=True: only the ones with connection changes between
-    rounds (dyn_*, which need updates_of), else only the static-topology ones."""
+    """Golden relay fixtures (hop / parent / per-round relays from the reference harness);
+    dynamic=True: only the ones with connection changes between rounds (dyn_*, which need
+    updates_of), else only the static-topology ones.  The real-TCP fixtures (config1_tcp,
+    tcp*) hold reachability only: tcp_cases()."""
     return sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith(".npz") and f.startswith(prefix)
-                  and f != "config1_tcp.npz" and f.startswith("dyn_") == dynamic)
+                  and not f.startswith(("config1_tcp", "tcp")) and f.startswith("dyn_") == dynamic)
+
+
+def tcp_cases():
+    """Real localhost-TCP runs of reference Nodes: reachability per (peer, msg) + relays."""
+    return sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith(".npz")
+                  and f.startswith(("config1_tcp", "tcp")))
+
+
+def wire_cases():
+    """Harness runs with the bytes every connection carried per round (wire_*)."""
+    return golden_cases("wire_")
+
+
+def fixture_streams(z):
+    """{round: {(sender, receiver): bytes}} of a wire_* fixture."""
+    out = {}
+    blob = z["s_blob"].tobytes()
+    off = z["s_off"]
+    for i, (r, a, b) in enumerate(zip(z["s_round"], z["s_sender"], z["s_receiver"])):
+        out.setdefault(int(r), {})[(int(a), int(b))] = blob[off[i]:off[i + 1]]
+    return out
+
+
+def deliveries_from_planes(hop, parent, r):
+    """Round r's first receipts (Deliveries, sorted by (peer, msg)) from hop/parent planes."""
+    import numpy as np
+    from p2pnetwork.gpu.network import Deliveries
+    vs, ms = np.nonzero(hop == r)
+    return Deliveries(vs.astype(np.int32), ms.astype(np.int32), np.full(len(vs), r, np.int32),
+                      parent[vs, ms].astype(np.int32))
 
 
 def updates_of(z):

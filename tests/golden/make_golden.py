@@ -32,6 +32,8 @@ Node.disconnect_with_node / node_disconnected and new NodeConnection pairs.
 
 Usage:  python tests/golden/make_golden.py        (writes tests/golden/*.npz)
         python tests/golden/make_golden.py dyn    (only the dyn_* fixtures)
+        python tests/golden/make_golden.py wire   (only the wire_* byte-stream fixtures)
+        python tests/golden/make_golden.py tcp    (only the larger real-TCP fixtures)
 """
 import os
 import sys
@@ -131,6 +133,7 @@ class Harness:
         self.churn_thr, self.cseed, self.msg_base = churn_thr, cseed, msg_base
         self.round = 0
         self.outbox = []
+        self.streams = []  # streams[r] = {(sender, receiver): bytes written in round r, arrived}
         RelayNode = make_node_class(Node)
         V = graph.V
         self.nodes = [RelayNode(i, self) for i in range(V)]
@@ -217,6 +220,9 @@ class Harness:
                 while i < len(batch) and batch[i][0] == rcv and batch[i][1] == snd:
                     buf += batch[i][3]
                     i += 1
+                while len(self.streams) < self.round:
+                    self.streams.append({})
+                self.streams[self.round - 1][(snd, rcv)] = buf
                 conn = self.conn[(rcv, snd)]
                 node = self.nodes[rcv]
                 pos = buf.find(eot)
@@ -289,6 +295,85 @@ def case(name, graph, M, src_seed, mode="flood", k=3, gseed=0, churn=0.0, cseed=
           f"{relays.sum() / dt:.0f} relays/s) -> {os.path.getsize(out)} B")
 
 
+def wire_case(name, graph, M, src_seed, mode="flood", k=3, gseed=0, churn=0.0, cseed=0):
+    """The bytes every connection carried, per round, in a harness run: the reference's own
+    NodeConnection.send framing of {"mid": m} payloads (JSON + EOT), in the order the
+    reference's Node objects wrote them.  Pins wire.StreamTap byte for byte."""
+    thr = int(np.floor(churn * 4294967296.0)) if churn else 0
+    src = make_sources(graph.V, M, seed=src_seed)
+    h = Harness(graph, mode, k, gseed, thr, cseed)
+    hop, parent, relays, recv = h.run(src)
+    rnd, snd, rcv, off, blob = [], [], [], [0], bytearray()
+    for r, st in enumerate(h.streams):
+        for (a, b), buf in sorted(st.items()):
+            rnd.append(r), snd.append(a), rcv.append(b)
+            blob += buf
+            off.append(len(blob))
+    out = os.path.join(HERE, f"{name}.npz")
+    np.savez_compressed(out, rowptr=graph.rowptr, colidx=graph.colidx, src=src, hop=hop, parent=parent,
+                        round_relays=relays, mode=np.array(mode), fanout=np.int64(k),
+                        gossip_seed=np.uint64(gseed), churn_threshold=np.uint64(thr),
+                        churn_seed=np.uint64(cseed), s_round=np.array(rnd, np.int32),
+                        s_sender=np.array(snd, np.int32), s_receiver=np.array(rcv, np.int32),
+                        s_off=np.array(off, np.int64), s_blob=np.frombuffer(bytes(blob), np.uint8))
+    print(f"{name}: {len(rnd)} streams, {len(blob)} bytes, relays={relays.sum()} -> {os.path.getsize(out)} B")
+
+
+def wire_cases():
+    wire_case("wire_ws60_flood_churn10", PeerGraph.watts_strogatz(60, 4, 0.2, seed=41), 8, 41,
+              churn=0.10, cseed=3)
+    wire_case("wire_ba80_gossip_k2", PeerGraph.barabasi_albert(80, 3, seed=42), 10, 42,
+              mode="gossip", k=2, gseed=19)
+
+
+def tcp_case(name, graph, src, settle=3.0):
+    """Real reference Nodes on localhost TCP (one per peer, connections dialled by the lower
+    id), len(src) concurrent floods through the dedup app.  TCP arrival order decides parents
+    and hops, so only reachability per (peer, message) and the total relay count (sum of
+    message_count_send) are recorded."""
+
+    class TcpRelay(Node):
+        def __init__(self, i, port):
+            super().__init__("127.0.0.1", port, id=str(i))
+            self.seen = set()
+            self.lock = __import__("threading").Lock()
+
+        def node_message(self, node, data):
+            with self.lock:  # hooks run on per-connection threads (nodeconnection.py:216)
+                if data["mid"] in self.seen:
+                    return
+                self.seen.add(data["mid"])
+            self.send_to_nodes(data, exclude=[node])
+
+    V = graph.V
+    base = 42000 + (os.getpid() % 200) * 100
+    nodes = [TcpRelay(i, base + i) for i in range(V)]
+    for n in nodes:
+        n.start()
+    time.sleep(0.5)
+    for a in range(V):
+        for b in graph.neighbours(a):
+            if b > a:
+                assert nodes[a].connect_with_node("127.0.0.1", base + int(b))
+    time.sleep(1.5)
+    links = sum(len(n.all_nodes) for n in nodes)
+    assert links == graph.nnz, (links, graph.nnz)
+    for m, s in enumerate(src):
+        nodes[int(s)].seen.add(m)
+    for m, s in enumerate(src):
+        nodes[int(s)].send_to_nodes({"mid": m})
+    time.sleep(settle)
+    reached = np.array([[m in n.seen for m in range(len(src))] for n in nodes])
+    relays = sum(n.message_count_send for n in nodes)
+    for n in nodes:
+        n.stop()
+    for n in nodes:
+        n.join()
+    np.savez_compressed(os.path.join(HERE, f"{name}.npz"), rowptr=graph.rowptr, colidx=graph.colidx,
+                        src=np.asarray(src, dtype=np.int32), reached=reached, relays=np.int64(relays))
+    print(f"{name}: V={V} E={graph.n_edges} M={len(src)} reached {reached.sum()}/{reached.size}, relays={relays}")
+
+
 def config1_tcp():
     """Config 1: 10 real reference Nodes on localhost TCP, ring + chords 0-3, 3-6, 6-9, one
     flood broadcast from node 0 through the same dedup app.  TCP arrival order decides
@@ -357,6 +442,12 @@ def main():
     if sys.argv[1:] == ["dyn"]:
         dynamic_cases()
         return
+    if sys.argv[1:] == ["wire"]:
+        wire_cases()
+        return
+    if sys.argv[1:] == ["tcp"]:
+        tcp_larger()
+        return
     # config 2: 1k-peer random 8-regular, 64 concurrent floods
     g2 = PeerGraph.random_regular(1000, 8, seed=1)
     case("c2_rrg1000_flood", g2, 64, src_seed=1)
@@ -384,6 +475,18 @@ def main():
     case("edge_components_gossip_k1", ge, 70, 0, src=srcs, mode="gossip", k=1, gseed=3)
     dynamic_cases()
     config1_tcp()
+    wire_cases()
+    tcp_larger()
+
+
+def tcp_larger():
+    """Beyond config 1: 48 real reference Nodes on TCP over a random 4-regular graph with six
+    concurrent floods, and a 40-peer small world with two isolated peers (unreached)."""
+    tcp_case("tcp48_rrg4_m6", PeerGraph.random_regular(48, 4, seed=51), make_sources(48, 6, seed=51))
+    g = PeerGraph.watts_strogatz(38, 4, 0.3, seed=52)
+    rows = np.repeat(np.arange(g.V), g.degree())
+    e = [(int(a), int(b)) for a, b in zip(rows, g.colidx) if a < b]
+    tcp_case("tcp40_ws_isolated_m4", PeerGraph.from_edges(40, e), np.array([0, 5, 39, 20], np.int32))
 
 
 if __name__ == "__main__":

@@ -126,7 +126,7 @@ def test_compat_gpu_connection_changes_match_reference_golden(name):
             add, rem = upd[rnd]
             for a, b in rem:
                 a, b = sorted((int(a), int(b)))
-                self.nodes[a].disconnect_with_node(self._conn[a][b])
+                self.nodes[a].disconnect_with_node(self.connection(a, b))
             for a, b in add:
                 a, b = sorted((int(a), int(b)))
                 assert self.nodes[a].connect_with_node(self.nodes[b].host, self.nodes[b].port)
@@ -158,3 +158,64 @@ def test_compat_gpu_connection_changes_match_reference_golden(name):
     assert events.count("outbound_node_disconnected") == events.count("inbound_node_disconnected") == n_rem
     assert events.count("node_disconnect_with_outbound_node") == n_rem
     net.close()
+
+
+def test_compat_second_run_relays_only_new_broadcasts():
+    """run() relays the broadcasts queued since the previous run(): nothing is replayed, so no
+    node_message fires twice for one payload and the counters are not double-counted."""
+    from p2pnetwork.gpu import PeerGraph
+    from p2pnetwork.gpu.compat import CompatNetwork
+    got = []
+
+    class App(dedup_app()):
+        def node_message(self, node, data):
+            got.append((self.id, data["mid"]))
+            super().node_message(node, data)
+
+    g = PeerGraph.from_edges(5, [(0, 1), (1, 2), (2, 3), (3, 4)])
+    net = CompatNetwork(g, App, engine_factory=MockEngine)
+    net.nodes[0].seen["a"] = (0, -1)
+    net.nodes[0].send_to_nodes({"mid": "a"})
+    net.run()
+    first = list(got)
+    assert sorted(first) == [("1", "a"), ("2", "a"), ("3", "a"), ("4", "a")]
+    sends = [n.message_count_send for n in net.nodes]
+    assert net.run() == []  # nothing new queued: nothing relayed
+    net.nodes[4].seen["b"] = (0, -1)
+    net.nodes[4].send_to_nodes({"mid": "b"})
+    net.run()
+    assert sorted(got[len(first):]) == [("0", "b"), ("1", "b"), ("2", "b"), ("3", "b")]
+    # second run: flood relays deg at the origin (4: 1), deg-1 elsewhere (1, 1, 1, 0)
+    assert [n.message_count_send - s for n, s in zip(net.nodes, sends)] == [0, 1, 1, 1, 1]
+
+
+def test_compat_repeated_disconnect_is_queued_once():
+    """Dropping the same connection twice in one round (e.g. from two node_message calls) is
+    harmless, as in the reference: one engine update, both ends see one disconnect."""
+    from p2pnetwork.gpu import PeerGraph
+    from p2pnetwork.gpu.compat import CompatNetwork, SimNode
+    events = []
+
+    def cb(event, main_node, connected_node, data):
+        events.append((event, main_node.id))
+
+    class Eng(MockEngine):
+        updates = []
+
+        def update_edges(self, add=(), remove=()):
+            Eng.updates.append((list(add), list(remove)))
+            self.graph = self.g = self.g.with_changes(add, remove)
+
+    g = PeerGraph.from_edges(3, [(0, 1), (1, 2)])
+    net = CompatNetwork(g, SimNode, node_kwargs={"callback": cb}, engine_factory=Eng)
+    c = net.connection(0, 1)
+    net.nodes[0].disconnect_with_node(c)
+    net.nodes[0].disconnect_with_node(c)
+    # disconnect + connect back in the same round cancel out
+    net.nodes[1].disconnect_with_node(net.connection(1, 2))
+    assert net.nodes[1].connect_with_node(net.nodes[2].host, net.nodes[2].port)
+    net._apply_changes()
+    assert Eng.updates == [([], [(0, 1)])]
+    assert events.count(("inbound_node_disconnected", "1")) == 1
+    assert events.count(("outbound_node_disconnected", "0")) == 1
+    assert [c.id for c in net.nodes[1].all_nodes] == ["2"]

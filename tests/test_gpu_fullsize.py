@@ -1,0 +1,109 @@
+"""Full-size GPU parity at BASELINE.json configurations, through the C-ABI.
+
+* Config 5 -- 100M-peer Watts-Strogatz k=8 beta=0.1, per-round edge-drop churn p=0.05, 4096
+  concurrent floods -- unpartitioned on ONE MI355X (seen + two frontier planes = 154 GB of
+  its 288 GB).  Checked: the relay identity over the whole seen plane (word by word, never a
+  51 GB host copy: p2pg_read_seen_word), reset determinism, words 0 and 63 of the 4096-run ==
+  the matching 64-broadcast runs, word 63 == the C oracle's delivered set and per-round
+  counters, and word 0's hop / parent planes == the C oracle's bit for bit (100M x 64).
+  Reference anchor: the relay of node.py:106-120 with the lost sends of
+  nodeconnection.py:123-126.
+* A 1M-peer Barabasi-Albert m=4 push-gossip with 4096 broadcasts (all 64 words through the
+  packed-E / fused / compact-flush paths): the whole seen plane and every per-round counter ==
+  the C oracle, in every push form.
+Each test prints nothing for up to ~2 minutes (graph generation and the CPU oracle)."""
+import numpy as np
+import pytest
+
+from oracle import coracle
+from test_gpu_parity import assert_rounds_equal
+
+pytestmark = pytest.mark.gpu
+
+CSEED, GSEED = 0xC0FFEE, 0x5EED  # bench.py's seeds
+
+
+@pytest.fixture(scope="module")
+def config5():
+    from p2pnetwork.gpu import PeerGraph, make_sources
+    from p2pnetwork.gpu.network import churn_threshold
+    g = PeerGraph.watts_strogatz(100_000_000, 8, 0.1, seed=1)
+    return g, make_sources(g.V, 4096, seed=1), churn_threshold(0.05)
+
+
+def c5_net(g, thr, **kw):
+    from p2pnetwork.gpu import GraphNetwork
+    return GraphNetwork(g, mode="flood", churn_threshold_value=thr, churn_seed=CSEED, **kw)
+
+
+def test_config5_full_size_flood_churn(config5):
+    g, src, thr = config5
+    M = len(src)
+    deg = g.degree()
+    with c5_net(g, thr) as net:
+        net.broadcast(src)
+        a = net.run()
+        pop = np.zeros(g.V, dtype=np.int64)  # |seen set| per peer, 64 words at a time
+        cols = {}
+        for w in range(M // 64):
+            col = net.seen_word(w)
+            pop += np.bitwise_count(col)
+            if w in (0, 63):
+                cols[w] = col
+            del col
+        net.reset()
+        b = net.run()
+    assert [r.as_dict() for r in a] == [r.as_dict() for r in b]
+    delivered = int(pop.sum())
+    assert delivered == sum(r.new_deliveries for r in a)
+    assert 0.99 * g.V * M < delivered <= g.V * M  # churn loses sends, not (on WS) whole peers
+    # every first receipt relays deg - 1 (the sender excluded), the origin deg: node.py:106-116
+    assert sum(r.relays for r in a) == int((pop * (deg - 1)).sum()) + M
+    del pop
+    for w, col in cols.items():
+        with c5_net(g, thr, msg_id_base=64 * w) as sub:
+            sub.broadcast(src[64 * w:64 * w + 64])
+            rounds = sub.run()
+            np.testing.assert_array_equal(sub.seen_word(0), col)
+    ora = coracle.run(g.rowptr, g.colidx, src[64 * 63:], "flood", churn_threshold=thr,
+                      churn_seed=CSEED, record=False, want_seen=True)
+    np.testing.assert_array_equal(ora.seen[:, 0], cols[63])
+    assert_rounds_equal(rounds, ora.rounds)
+
+
+def test_config5_word0_hop_parent_match_c_oracle(config5):
+    """Messages 0..63 of config 5: first-receipt round and lowest-id surviving sender of all
+    100M peers, bit for bit against the C oracle (which re-draws every churn decision)."""
+    g, src, thr = config5
+    with c5_net(g, thr, record=True) as net:
+        net.broadcast(src[:64])
+        rounds = net.run()
+        hop, parent = net.hop_parent()
+    ora = coracle.run(g.rowptr, g.colidx, src[:64], "flood", churn_threshold=thr, churn_seed=CSEED,
+                      record=True)
+    assert_rounds_equal(rounds, ora.rounds)
+    assert np.array_equal(hop, ora.hop)
+    del hop, ora.hop
+    assert np.array_equal(parent, ora.parent)
+
+
+@pytest.mark.parametrize("push", ["auto", "atomic", "store_unfused"])
+def test_gossip_full_width_1m_matches_c_oracle(push, monkeypatch):
+    """1M-peer BA m=4, 4096 push-gossips, k=3: the whole seen plane (all 64 words) and every
+    per-round counter equal the C oracle's -- auto (dense rounds fused, packed E, compact
+    flush), row atomics only, and edge stores with separate pull / scatter passes."""
+    from p2pnetwork.gpu import GraphNetwork, PeerGraph, make_sources
+    monkeypatch.setenv("P2PG_GOSSIP_PUSH", "auto" if push == "auto" else push.split("_")[0])
+    monkeypatch.setenv("P2PG_FUSED", "0" if push == "store_unfused" else "1")
+    g = PeerGraph.barabasi_albert(1_000_000, 4, seed=5)
+    src = make_sources(g.V, 4096, seed=5)
+    with GraphNetwork(g, mode="gossip", fanout=3, gossip_seed=GSEED) as net:
+        net.broadcast(src)
+        rounds = net.run()
+        seen = net.seen_plane()
+    forms = {r.push_form for r in rounds if r.new_deliveries}
+    if push == "auto":
+        assert 3 in forms and 1 in forms, forms  # fused dense rounds and atomic sparse rounds
+    ora = coracle.run(g.rowptr, g.colidx, src, "gossip", 3, GSEED, record=False, want_seen=True)
+    np.testing.assert_array_equal(seen, ora.seen)
+    assert_rounds_equal(rounds, ora.rounds)

@@ -7,7 +7,7 @@ import zlib
 import numpy as np
 import pytest
 
-from conftest import golden_cases, load_golden, trim_zeros
+from conftest import fixture_streams, golden_cases, load_golden, tcp_cases, trim_zeros, wire_cases
 from oracle import philox, relay_oracle
 
 pytestmark = pytest.mark.gpu
@@ -323,3 +323,48 @@ def test_gpu_gossip_push_forms_match_oracle(kind, p, M, thr, fanout, push, monke
     np.testing.assert_array_equal(hop, ora.hop)
     np.testing.assert_array_equal(parent, ora.parent)
     assert_rounds_equal(rounds, ora.rounds)
+
+
+@pytest.mark.parametrize("name", tcp_cases())
+def test_gpu_matches_real_tcp_runs(name):
+    """The HIP engine on the topologies of the real localhost-TCP runs of reference Nodes
+    (config 1: ring + chords, one flood; 48 Nodes x 6 concurrent floods; a small world with
+    isolated peers): the delivered (peer, msg) set equals what TCP delivered and the relay
+    count equals the sum of message_count_send (examples/my_own_p2p_application.py:28-34,
+    node.py:106-120)."""
+    z = load_golden(name)
+    with gpu_net(z, "flood", record=False) as net:
+        net.broadcast(z["src"])
+        rounds = net.run()
+        delivered = net.delivered()
+    np.testing.assert_array_equal(delivered, z["reached"].reshape(delivered.shape))
+    assert sum(r.relays for r in rounds) == int(z["relays"])
+    if name == "config1_tcp":
+        assert int(z["relays"]) == 17 and delivered.all()
+
+
+@pytest.mark.parametrize("name", wire_cases())
+def test_gpu_deliveries_give_reference_wire_bytes(name):
+    """GPU deliveries (GraphNetwork.deliveries per round) -> wire.StreamTap -> the bytes the
+    reference's NodeConnection.send wrote on every connection, round by round."""
+    from p2pnetwork.gpu import GraphNetwork, PeerGraph
+    from p2pnetwork.gpu.wire import StreamTap
+    z = load_golden(name)
+    g = PeerGraph(z["rowptr"], z["colidx"])
+    M = len(z["src"])
+    kw = dict(mode=str(z["mode"]), fanout=int(z["fanout"]), gossip_seed=int(z["gossip_seed"]),
+              churn_threshold=int(z["churn_threshold"]), churn_seed=int(z["churn_seed"]))
+    tap = StreamTap(g, [{"mid": m} for m in range(M)], **kw)
+    want = fixture_streams(z)
+    got = {}
+
+    class Tapped(GraphNetwork):
+        def node_message_batch(self, d):
+            got[len(got)] = tap.feed(d)[0]
+
+    with Tapped(g, mode=kw["mode"], fanout=kw["fanout"], gossip_seed=kw["gossip_seed"],
+                churn_threshold_value=kw["churn_threshold"], churn_seed=kw["churn_seed"]) as net:
+        net.broadcast(z["src"])
+        net.run()
+    for r in range(max(len(got), max(want) + 1)):
+        assert got.get(r, {}) == want.get(r, {}), r

@@ -30,7 +30,7 @@ class ThreadTransport:
     def alltoall_rows(self, send, send_counts, recv_counts, W):
         import torch
         from p2pnetwork.gpu.partition import expand_rows, live_rows
-        torch.cuda.synchronize()
+        # no extra synchronisation: the production ordering (PartitionedNetwork._ready) is tested
         if self.sparse:  # the TorchTransport protocol: row flags + live rows only
             mask, rows, live = live_rows(send, send_counts, W)
             items = self._gather((mask, rows, np.asarray(send_counts), live))
@@ -42,7 +42,6 @@ class ThreadTransport:
                 rp.append(r[loff:loff + int(lv[self.rank]) * W])
             out = expand_rows(torch.cat(mp), torch.cat(rp), W)
             assert out.numel() == int(np.sum(recv_counts)) * W
-            torch.cuda.synchronize()
             return out
         items = self._gather((send, np.asarray(send_counts)))
         pieces = []
@@ -51,7 +50,6 @@ class ThreadTransport:
             pieces.append(buf[off:off + int(counts[self.rank]) * W])
         out = torch.cat(pieces) if pieces else send[:0]
         assert out.numel() == int(np.sum(recv_counts)) * W
-        torch.cuda.synchronize()
         return out
 
     def allreduce_sum(self, values):

@@ -5,7 +5,7 @@ Node.message_count_send, p2pnetwork/node.py:116)."""
 import numpy as np
 import pytest
 
-from conftest import golden_cases, load_golden, trim_zeros, updates_of
+from conftest import golden_cases, load_golden, tcp_cases, trim_zeros, updates_of
 from oracle import relay_oracle
 
 
@@ -75,6 +75,17 @@ def test_config1_tcp_reachability():
     res = relay_oracle.flood(z["rowptr"], z["colidx"], z["src"])
     np.testing.assert_array_equal(res.delivered()[:, 0], z["reached"])
     assert res.total_relays == int(z["relays"]) == 17
+
+
+@pytest.mark.parametrize("name", tcp_cases())
+def test_oracle_matches_real_tcp_runs(name):
+    """Every real-TCP fixture (config 1, 48 Nodes x 6 concurrent floods, a small world with
+    isolated peers): delivered (peer, msg) set and total relays agree."""
+    z = load_golden(name)
+    res = relay_oracle.flood(z["rowptr"], z["colidx"], z["src"])
+    reached = z["reached"].reshape(len(z["rowptr"]) - 1, -1)
+    np.testing.assert_array_equal(res.delivered(), reached)
+    assert res.total_relays == int(z["relays"])
 
 
 @pytest.mark.parametrize("name", golden_cases())
