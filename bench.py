@@ -9,13 +9,17 @@ Barabasi-Albert (m=4) graph, 4096 concurrent push-gossip broadcasts with fanout 
 picks), synthetic graph and origins (no datasets).  A "step" = one complete broadcast: reset
 of the per-run state + every round until quiescence, graph resident in HBM.
 
-Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): broadcasts
-are independent, so each rank runs its own 4096 broadcasts (global message ids
-rank*4096 + m: different origins and Philox streams) on its own replica of the graph -- weak
-scaling with no data-path collective; value = relays of all ranks / max-over-ranks time.
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): the SAME
+4096 broadcasts are split across the ranks by message word (rank r runs messages
+r*4096/N .. (r+1)*4096/N - 1, global message ids, so origins and Philox streams are those of the
+1-GPU run) on a replica of the graph -- strong scaling (fixed total work), no data-path
+collective, because broadcasts are independent bit lanes; value = relays of all ranks /
+max-over-ranks time.  Config 5 (--workload c5) is vertex-partitioned instead (RCCL all-to-all of
+boundary rows), and runs unpartitioned at N = 1.
 
 Prints ONE JSON line (rank 0) with the driver's fields plus "roofline" (dominant kernel,
-algorithmic bytes / its HIP-event time) and "cpu_baseline" (the C oracle on host cores).
+algorithmic bytes / its HIP-event time) and "cpu_baseline" (two CPU legs on the host cores: the
+C/OpenMP oracle and the 1-core object-level relay simulator).
 """
 import argparse
 import json
@@ -126,6 +130,23 @@ def survey_bytes(rounds, mode):
     return tot
 
 
+def survey_bytes_kernel(rounds, mode, kclass):
+    """SURVEY.md 8d bytes of the rounds whose arrivals kernel class `kclass` consumes (the
+    fused kernel pulls round r's arrivals: B_r with round r-1's relays)."""
+    if mode == "flood":
+        return survey_bytes(rounds, mode) if kclass == "flood_pull" else 0
+    forms = push_forms(rounds)
+    tot = 0
+    for i in range(1, len(rounds)):
+        consumer = ("gossip_fused" if forms[i] == FUSED else
+                    "gossip_pull" if forms[i - 1] in (EDGE, FUSED) else "gossip_update")
+        if consumer != kclass:
+            continue
+        p, r = rounds[i - 1], rounds[i]
+        tot += 8 * p.relays + 8 * p.active_words + 4 * p.deg_active + 8 * p.active_vertices + 24 * r.active_words
+    return tot
+
+
 def build_graph(w):
     from p2pnetwork.gpu import PeerGraph
     if w["graph"] == "ba":
@@ -139,10 +160,26 @@ def build_graph(w):
     raise ValueError(w["graph"])
 
 
-def cpu_baseline(g, w, src, sample_msgs, thr):
-    """The C oracle (oracle/relay_oracle.c, OpenMP) on a bounded sample of the same workload:
-    the same graph with the first `sample_msgs` broadcasts.  Reported, not a target."""
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(g, w, src, sample_msgs, thr, object_seconds=10.0):
+    """Two CPU legs on a bounded sample of the same workload (reported, not a target):
+    (ii) the C oracle (oracle/relay_oracle.c, OpenMP, every host thread) on the same graph with
+    the first `sample_msgs` broadcasts -- the headline cpu_baseline value; (i) the 1-core,
+    object-level Python relay (oracle/object_relay.py: Node / NodeConnection-shaped objects, JSON
+    + EOT framing per send, the reference's per-relay work) on broadcast 0 until ~object_seconds
+    of relays have been made (a partial broadcast: the rate per relay is what is sampled)."""
     from oracle import coracle
+    from oracle.object_relay import ObjectRelay
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
     os.environ["OMP_NUM_THREADS"] = str(threads)
     s = src[:sample_msgs]
@@ -151,9 +188,27 @@ def cpu_baseline(g, w, src, sample_msgs, thr):
                       record=False)
     dt = time.perf_counter() - t0
     relays = sum(r["relays"] for r in res.rounds)
-    return {"value": relays / dt / 1e9, "unit": "GTEPS", "cores": threads, "kind": "port",
-            "sample": f"{sample_msgs} of {w['M']} broadcasts on the full {w['V']}-peer graph: "
-                      f"{relays} relays in {dt:.2f} s (oracle/relay_oracle.c, {threads} OpenMP threads)"}
+    c_leg = {"value": relays / dt / 1e9, "unit": "GTEPS", "cores": threads, "kind": "port",
+             "sample": f"{sample_msgs} of {w['M']} broadcasts on the full {w['V']}-peer graph: "
+                       f"{relays} relays in {dt:.2f} s (oracle/relay_oracle.c, {threads} OpenMP threads)"}
+    # object leg: calibrate the relay budget on a short run, then time ~object_seconds
+    sim = ObjectRelay(g.rowptr, g.colidx, w["mode"], w["fanout"], GOSSIP_SEED, thr, CHURN_SEED)
+    t0 = time.perf_counter()
+    probe = sum(sim.run(src[:1], max_relays=20000))
+    rate = probe / max(time.perf_counter() - t0, 1e-6)
+    sim = ObjectRelay(g.rowptr, g.colidx, w["mode"], w["fanout"], GOSSIP_SEED, thr, CHURN_SEED)
+    t0 = time.perf_counter()
+    per_round = sim.run(src[:1], max_relays=int(rate * object_seconds))
+    odt = time.perf_counter() - t0
+    orel = sum(per_round)
+    o_leg = {"value": orel / odt / 1e9, "unit": "GTEPS", "cores": 1, "kind": "port",
+             "sample": f"broadcast 0 of {w['M']} on the full {w['V']}-peer graph, its first "
+                       f"{orel} relays ({len(per_round)} rounds) in {odt:.2f} s (oracle/object_relay.py, "
+                       f"1 Python thread, {len(sim.peers)} peer objects)"}
+    out = dict(c_leg)
+    out["cpu_model"] = cpu_model()
+    out["legs"] = {"c_openmp": c_leg, "python_objects_1core": o_leg}
+    return out
 
 
 def load_traffic(workload, kernel):
@@ -177,6 +232,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--peers", type=int, default=0, help="override the workload's peer count "
                     "(rehearsals only; the reported workload names the size actually run)")
+    ap.add_argument("--msgs", type=int, default=0, help="override the workload's broadcast count "
+                    "(rehearsals only, e.g. one rank's share of a split; the reported workload names it)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo stages the exchange through host memory (rehearsal with several "
                          "ranks on one GPU); nccl = RCCL over xGMI")
@@ -202,6 +259,9 @@ def main():
     if args.peers:
         w["V"] = args.peers
         w["name"] += f" [REDUCED: {args.peers} peers]"
+    if args.msgs:
+        w["M"] = args.msgs
+        w["name"] += f" [REDUCED: {args.msgs} broadcasts]"
     thr = churn_threshold(w.get("churn", 0.0))
     partitioned = bool(w.get("partition")) and world > 1
     t_gen = time.perf_counter()
@@ -216,9 +276,13 @@ def main():
         src = make_sources(g.V, M, seed=1)
         net = PartitionedNetwork(g, world, rank, TorchTransport(device=torch.device("cuda", local)), **common)
     else:
-        # message-axis replicas: rank r runs broadcasts r*M .. r*M+M-1 on its own graph copy
-        src = make_sources(g.V, M, seed=1, msg_id_base=rank * M)
-        net = GraphNetwork(g, msg_id_base=rank * M, **common)
+        # message axis, fixed total work: rank r runs broadcasts [lo, hi) of the M (global ids,
+        # so origins and Philox streams are the 1-GPU run's) on its own graph copy
+        if M % (64 * world):
+            raise SystemExit(f"--gpus {world}: {M} broadcasts do not split into whole 64-bit words")
+        lo, hi = rank * M // world, (rank + 1) * M // world
+        src = make_sources(g.V, M, seed=1)[lo:hi]
+        net = GraphNetwork(g, msg_id_base=lo, **common)
     net.broadcast(src)
     for _ in range(args.warmup):
         net.reset()
@@ -249,7 +313,7 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=red)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        if not partitioned:  # replicas: sum the ranks' relays (partitioned counters are global)
+        if not partitioned:  # message split: sum the ranks' relays (partitioned counters are global)
             r = torch.tensor([relays], dtype=torch.float64, device=red)
             dist.all_reduce(r, op=dist.ReduceOp.SUM)
             relays = int(r.item())
@@ -257,11 +321,14 @@ def main():
 
     last = all_rounds[-1]
     local_last = net.local_rounds if partitioned else last  # this rank's kernels' work
-    mb = model_bytes(local_last, w["mode"], (M + 63) // 64)
+    W_local = (len(src) + 63) // 64 if not partitioned else (M + 63) // 64
+    mb = model_bytes(local_last, w["mode"], W_local)
     dominant = max(KCLASS, key=lambda k: kt[k][0])
     dom_ms, dom_n = kt[dominant]
     achieved = mb[dominant] / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
     traffic = load_traffic(args.workload, dominant)
+    sb_step = survey_bytes(local_last, w["mode"])
+    sb_dom = survey_bytes_kernel(local_last, w["mode"], dominant)
     kernel_ms_total = sum(v[0] for v in kt.values())
     out = {
         "metric": "msg-edge relays/sec (GTEPS) at 10M peers x 4096 msgs; % HBM roofline",
@@ -272,17 +339,18 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "strong" if w.get("partition") else "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "u64",
         "data": "synthetic (generated graph + Philox origins)",
         "config": {"workload": w["name"], "peers": g.V, "edges": g.n_edges,
-                   "broadcasts": M if w.get("partition") else M * world,
+                   "broadcasts": M,
                    "mode": w["mode"], "fanout": w["fanout"], "churn": w.get("churn", 0.0),
                    "rounds": len(last),
                    "parallelism": (f"vertex partition x{world} (RCCL all-to-all of boundary rows)"
                                    if partitioned else
-                                   f"message-axis replicas x{world}" if world > 1 else "single GPU")},
+                                   f"message-axis split x{world} ({M // world} broadcasts per rank)"
+                                   if world > 1 else "single GPU")},
         "roofline": {
             "bound": "hbm",
             "kernel": dominant,
@@ -294,11 +362,15 @@ def main():
             "algorithmic_bytes_per_launch": mb[dominant] / max(dom_n, 1),
             "avg_launch_ms": dom_ms / max(dom_n, 1),
             "launches_per_step": dom_n,
+            # SURVEY.md 8(d)'s own byte model (gossip: 8 B per bit relay) for the rounds whose
+            # arrivals this kernel consumes, over the same kernel time
+            "frac_survey_model": (sb_dom / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS) if dom_ms > 0 else 0.0,
         },
         "kernel_ms_per_step": {k: v[0] for k, v in kt.items()},
         "model_bytes_per_step": mb,
         "whole_step_model_GBps": sum(mb.values()) / (elapsed / args.steps) / 1e9,
-        "survey_model_bytes_per_step": survey_bytes(last, w["mode"]),
+        "survey_model_bytes_per_step": sb_step,
+        "whole_step_frac_survey_model": sb_step / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBPS,
         "kernel_time_frac_of_step": kernel_ms_total / (elapsed / args.steps * 1e3),
         "relays_per_step_per_gpu": relays / args.steps / world,
         "exchange_ms_per_step": (net.exchange_s * 1e3) if partitioned else 0.0,
