@@ -61,6 +61,9 @@ struct p2pg_engine {
   bool last_push_e = false;    // gossip: pushes of the previous round went to E (dense)
   double e_thresh = 0.04;      // store-mode when active words >= thresh * active rows * W
                                // (c4 A/B, interleaved runs: 0.04 320.4 ms vs 0.1 324.3 ms)
+  double v_thresh = 0.3;       // ... and active rows >= v_thresh * V: a dense round visits every
+                               // unsaturated peer, a sparse one only the pushed-to rows (narrow
+                               // rows: word density alone is high whenever anything is active)
   int push_mode = 0;           // 0 auto, 1 always row atomics, 2 always edge stores
   bool fused = true;           // dense rounds after dense rounds: one pull+scatter pass
   uint64_t prev_aw = 0, prev_av = 0;  // active words / rows of the previous round
@@ -301,7 +304,7 @@ int alloc_state(p2pg_engine* e) {
     }
   }
   if ((rc = A((void**)&s.S, e->bm_bytes))) return rc;
-  if (gossip && e->W <= 64)  // packed E rows (see DevState::AW)
+  if (gossip && e->W > PACK_W_MAX_PLAIN && e->W <= 64)  // packed E rows (see DevState::AW)
     for (int i = 0; i < 2; ++i)
       if ((rc = A((void**)&s.AW[i], sizeof(uint64_t) * (size_t)e->V))) return rc;
   if ((rc = alloc_edge_planes(e))) {
@@ -343,6 +346,7 @@ int p2pg_create(const p2pg_config* cfg, p2pg_engine** out) {
   p2pg_engine* e = new p2pg_engine;
   e->cfg = *cfg;
   if (const char* t = std::getenv("P2PG_E_THRESH")) e->e_thresh = std::atof(t);
+  if (const char* t = std::getenv("P2PG_V_THRESH")) e->v_thresh = std::atof(t);
   if (const char* f = std::getenv("P2PG_FUSED")) e->fused = std::strcmp(f, "0") != 0;
   if (const char* m = std::getenv("P2PG_GOSSIP_PUSH"))
     e->push_mode = !std::strcmp(m, "atomic") ? 1 : (!std::strcmp(m, "store") ? 2 : 0);
@@ -602,8 +606,9 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
     // the push form, never the result), the same pass also pushes this round's receipts.
     const bool dense_pred = e->push_mode == 2 ||
         (e->push_mode == 0 && e->prev_av > 0 &&
-         (double)e->prev_aw >= e->e_thresh * (double)e->prev_av * (double)e->W);
-    fused_round = s.E[1] != s.E[0] && s.AW[0] && e->W <= 64 && !e->d_gid && dense_pred;
+         (double)e->prev_aw >= e->e_thresh * (double)e->prev_av * (double)e->W &&
+         (double)e->prev_av >= e->v_thresh * (double)e->V);
+    fused_round = !e->d_gid && dense_pred && gossip_fused_supported(s);
     if (fused_round) {
       if ((rc = timed(e, 7, [&] {
              return launch_gossip_fused(g, s, p, e->hp, e->d_hub_big, e->n_hub_big, e->stream);
@@ -652,7 +657,8 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
       } else if (e->push_mode == 0) {
         if ((rc = read_stats())) return rc;
         use_e = (double)tot[ST_ACTIVE_W] >=
-                e->e_thresh * (double)tot[ST_ACTIVE_V] * (double)e->W && tot[ST_ACTIVE_V] > 0;
+                e->e_thresh * (double)tot[ST_ACTIVE_V] * (double)e->W && tot[ST_ACTIVE_V] > 0 &&
+                (double)tot[ST_ACTIVE_V] >= e->v_thresh * (double)e->V;
       }
     }
     if ((rc = timed(e, use_e ? 6 : 2, [&] {

@@ -1,0 +1,466 @@
+// Gossip fused dense round for narrow rows (W <= 32 words = up to 2048 concurrent
+// broadcasts): several peers per wave.
+//
+// Why: the fused kernel of relay_kernels.hip (k_gossip_fused) maps one peer row to one wave,
+// lane = word.  At W = 64 that is one coalesced 512 B row per wave; at W = 8 (one rank's share
+// when the 4096 broadcasts of config 4 are split over 8 GPUs) 56 of its 64 lanes idle and every
+// peer still costs a whole wave visit, so a step took as long as the W = 64 step (250 vs 294
+// ms, profiles/r02/bench_c4_m512_v15.json).  Here a wave takes a BATCH of consecutive peers:
+//   lane = (batch peer g, word w), g = lane / WP, w = lane % WP, WP = W rounded up to a power
+//   of two, at most 64 / WP peers and at most 64 adjacency slots per batch (or one wider peer);
+// so a batch's seen / frontier rows are one contiguous run of memory, its adjacency slots one
+// contiguous range of colidx / rev (peers are consecutive), and the per-peer fixed work (row
+// offsets, neighbour ids, activity words, the pick loop, the flush) is shared by the batch.
+//
+// Per batch (same results as k_gossip_fused):
+//   1. gather: for every adjacency slot j of the batch (lane = slot, 64 per window) whose
+//      neighbour v was active in round r-1 (A bit, churn of round r-1 applied), the owner peer's
+//      lanes load E row j (receiver-major: what v pushed to that peer in round r-1; packed when
+//      W > PACK_W_MAX_PLAIN: word w at position popcount(AW[v] & below w), else whole) -- the
+//      slot index and v's word mask reach the owner's lanes by ds_bpermute;
+//   2. dedup against seen, new frontier row, AW mask, A / S bits, counters;
+//   3. picks: the new (peer, message) bits are compacted into an LDS list, lanes evaluate
+//      Philox + Floyd (gossip_picks_t) and OR the message bit into an LDS table indexed by
+//      (batch slot, word); then the flush stores, for every batch slot and every active word
+//      of its peer, the table word into the RECEIVER's packed E row of the connection
+//      (rev[slot]), zeros included (receivers gather by the sender's AW mask).
+// Hubs (deg > HUB_T) are left to the hub kernels, as in k_gossip_fused.
+#include "device_util.h"
+
+namespace p2pg {
+namespace {
+
+constexpr int GLIST_G = 1024;  // new bits listed per pick pass (a peak-round batch: ~700)
+
+template <int LW>
+struct GroupedLds {
+  static constexpr int WP = 1 << LW;
+  // table slots: 512 (slot, word) masks (4 KB), 64 slots at most; a batch spans at most TS
+  // slots (one wider peer: several pick windows), so ~6.5 KB of LDS per wave allows 4 waves
+  // per SIMD
+  static constexpr int TS = (512 >> LW) < 64 ? (512 >> LW) : 64;
+  alignas(8) uint32_t tbl[TS][WP][2];  // (slot, word) mask as two 32-bit halves (LDS atomics)
+  uint16_t lst[GLIST_G];               // new bits: lane << 6 | bit
+  int32_t off[36];                     // batch peer i -> first slot of its row, batch-relative
+  uint32_t wmask[32];                  // batch peer i -> active words of its new frontier row
+  uint8_t owner[64];                   // pick-window slot -> batch peer
+};
+
+// Lane-varying register read (ds_bpermute).  Every call site runs with the whole wave active:
+// a disabled source lane would not deliver its value.
+__device__ __forceinline__ uint32_t bperm(int src_lane, uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane << 2, (int)x);
+}
+
+__device__ __forceinline__ uint64_t bperm64(int src_lane, uint64_t x) {
+  return ((uint64_t)bperm(src_lane, (uint32_t)(x >> 32)) << 32) | bperm(src_lane, (uint32_t)x);
+}
+
+// lane-varying read of lane src's 64-bit value
+__device__ __forceinline__ int64_t readlane64_v(int64_t x, int src_lane) {
+  return (int64_t)bperm64(src_lane, (uint64_t)x);
+}
+
+__device__ __forceinline__ uint64_t bits_between(int lo, int hi) {  // bits [lo, hi), 0 <= lo, hi <= 64
+  const uint64_t below_hi = hi >= 64 ? ~0ull : ((1ull << hi) - 1ull);
+  const uint64_t below_lo = lo >= 64 ? ~0ull : ((1ull << lo) - 1ull);
+  return hi > lo ? below_hi & ~below_lo : 0ull;
+}
+
+// One batch's registers as it moves through the software pipeline (see the kernel).
+struct GStage {
+  int b0, n;          // task peers b0 .. b0+n-1 (n = 0: no batch)
+  int64_t rb0, rb1;   // its adjacency slot range
+  uint64_t s;         // lane (g, w): seen word
+  int32_t v;          // lane = slot of the first 64: neighbour id ...
+  uint32_t rv;        // ... the receiver's slot of the connection (rev) ...
+  uint32_t aword;     // ... the neighbour's activity word (round r-1) ...
+  uint64_t amv;       // ... and its active-word mask
+  bool rcv;           // slot exists and its owner peer is processed
+  uint64_t mr;        // lane (g, w): active slots of the first 64 not yet gathered
+};
+
+#ifndef P2PG_GROUPED_WAVES
+#define P2PG_GROUPED_WAVES 4  // <= 128 VGPRs
+#endif
+template <bool CHURN, int K, int LW>
+__global__ __launch_bounds__(256, P2PG_GROUPED_WAVES) void k_gossip_fused_grouped(DevGraph g, DevState st, RoundParams p) {
+  using Lds = GroupedLds<LW>;
+  constexpr int WP = Lds::WP;
+  constexpr int TS = Lds::TS;
+  constexpr int GMAX = (64 >> LW) < 32 ? (64 >> LW) : 32;  // peers per batch
+  constexpr int SPI = 64 / WP;                              // flush: slots per instruction
+  constexpr int KK = K > 0 ? K : 16;
+  __shared__ Lds lds[WPB];
+  const int lane = threadIdx.x & 63;
+  Lds& L = lds[wave_in_block()];
+  const int64_t V = g.V;
+  const int W = st.W;
+  const int cur = p.round & 1, prv = cur ^ 1;
+  const uint64_t* __restrict__ Src = st.E[prv];
+  uint64_t* __restrict__ Eo = st.E[cur];
+  uint64_t* __restrict__ Fc = st.F[cur];
+  const uint32_t* __restrict__ Ap = st.A[prv];
+  const uint64_t* __restrict__ AWp = st.AW[prv];
+  // packed E rows (sender's active words only, positions from AW) when AW planes exist --
+  // W > PACK_W_MAX_PLAIN; narrower rows are stored whole, zeros included, so that a receiver
+  // needs no random 8 B read of the sender's word mask per connection
+  const bool packed = AWp != nullptr;
+  const int k = K > 0 ? K : p.fanout;
+  const int gl = lane >> LW;        // this lane's batch peer
+  const int wl = lane & (WP - 1);   // this lane's word
+  const bool wvalid = wl < W;
+  const uint64_t fm = wvalid ? full_mask(wl, W, st.M) : 0ull;
+  const uint64_t gmask = (1ull << WP) - 1ull;
+  const int64_t ntasks = (V + 31) >> 5;
+  uint64_t tot[STAT_N] = {0, 0, 0, 0, 0, 0, 0, 0};
+
+  for (int64_t task = (int64_t)blockIdx.x * WPB + wave_in_block(); task < ntasks;
+       task += (int64_t)gridDim.x * WPB) {
+    const int64_t u0 = task << 5;
+    const uint32_t sat0 = st.S[task];
+    const int nv = V - u0 < 32 ? (int)(V - u0) : 32;
+    uint32_t todo = ~sat0;
+    if (g.H) todo &= ~g.H[task];  // hubs: k_pull_hub_* and the chunk-item scatter
+    if (nv < 32) todo &= (1u << nv) - 1u;
+    if (!todo) {
+      if (lane == 0) st.A[cur][task] = 0u;
+      continue;
+    }
+    int64_t rp = 0;
+    if (lane <= nv) rp = g.rowptr[u0 + lane];
+    uint32_t c[STAT_N] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t aw = 0, sat = sat0;
+    uint32_t rest = todo;
+
+    // ---- pipeline stages (software pipeline over the task's batches, as in k_gossip_fused:
+    // rows of t+3, activity of t+2, first gathers of t+1 are in flight while t is consumed)
+    auto rows = [&](GStage& q) {
+      q.n = 0;
+      q.rcv = false;
+      q.s = 0;
+      q.v = 0;
+      q.rv = 0;
+      if (!rest) return;
+      // the batch: <= GMAX consecutive peers and <= TS slots, or one wider peer
+      const int b0 = __builtin_ctz(rest);
+      const int64_t rb0 = readlane64(rp, b0);
+      const bool fits = lane > b0 && lane <= b0 + GMAX && lane <= nv && rp - rb0 <= TS;
+      const int cnt = __popcll(__ballot(fits));
+      const int n = cnt > 0 ? cnt : 1;
+      rest &= (b0 + n >= 32 ? 0u : ~0u << (b0 + n));
+      q.b0 = b0;
+      q.n = n;
+      q.rb0 = rb0;
+      q.rb1 = readlane64(rp, b0 + n);
+      const bool mine = gl < n && ((todo >> (b0 + gl)) & 1u);
+      if (mine && wvalid) q.s = ld_once(&st.seen[(u0 + b0 + gl) * W + wl]);
+      int gj = 0;  // batch peer owning slot rb0 + lane
+      for (int i = 1; i < n; ++i) gj += readlane64(rp, b0 + i) - rb0 <= (int64_t)lane;
+      q.rcv = rb0 + lane < q.rb1 && ((todo >> (b0 + gj)) & 1u);
+      if (q.rcv) {
+        q.v = ld_once(&g.colidx[rb0 + lane]);
+        q.rv = ld_once(&g.rev[rb0 + lane]);
+      }
+    };
+    auto activity = [&](GStage& q) {
+      q.aword = 0;
+      q.amv = 0;
+      if (q.rcv) {
+        q.aword = Ap[q.v >> 5];
+        if (packed) q.amv = AWp[q.v];
+      }
+    };
+    // lane (g, w): need = words of peer g still open; the owner's slot range within 64 lanes
+    auto need_of = [&](const GStage& q) -> uint64_t {
+      const bool mine = gl < q.n && ((todo >> (q.b0 + gl)) & 1u);
+      return mine ? fm & ~q.s : 0ull;
+    };
+    auto my_slots = [&](const GStage& q, int64_t cb) -> uint64_t {
+      const int bi = gl < q.n ? q.b0 + gl : q.b0;
+      const int64_t lo = readlane64_v(rp, bi) - cb, hi = readlane64_v(rp, bi + 1) - cb;
+      return bits_between(lo < 0 ? 0 : (lo > 64 ? 64 : (int)lo), hi < 0 ? 0 : (hi > 64 ? 64 : (int)hi));
+    };
+    uint64_t X[4];
+    auto gathers = [&](int64_t cb, uint64_t& mg, uint64_t amv) {
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const bool ok = mg != 0ull;
+        const int idx = ok ? __builtin_ctzll(mg) : 0;
+        mg &= mg - 1ull;
+        bool here = ok;
+        int pos = wl;
+        if (packed) {  // uniform branch
+          const uint64_t a = bperm64(idx, amv);  // the sender's active-word mask
+          here = ok && ((a >> wl) & 1ull);
+          pos = __popcll(a & ((1ull << wl) - 1ull));
+        }
+        X[qq] = here ? __builtin_nontemporal_load(&Src[(cb + idx) * W + pos]) : 0ull;
+      }
+    };
+    auto active_slots = [&](const GStage& q, int64_t cb, int32_t v, bool rcv, uint32_t aword) -> uint64_t {
+      bool act = rcv && ((aword >> (v & 31)) & 1u);
+      if (CHURN && act) {
+        int gj = 0;
+        for (int i = 1; i < q.n; ++i) gj += readlane64(rp, q.b0 + i) <= cb + lane;
+        act = !churn_dropped((uint32_t)(p.round - 1), gidx(g, u0 + q.b0 + gj), gidx(g, v), p.churn_thr,
+                             p.cseed_lo, p.cseed_hi);
+      }
+      return __ballot(act);
+    };
+    auto first_gathers = [&](GStage& q) {
+      q.mr = 0;
+      X[0] = X[1] = X[2] = X[3] = 0ull;
+      if (q.n == 0) return;
+      const uint64_t need = need_of(q);
+      const uint64_t am = active_slots(q, q.rb0, q.v, q.rcv, q.aword);
+      const uint64_t ms = my_slots(q, q.rb0);  // ds_bpermute: evaluated by every lane
+      uint64_t mg = need ? am & ms : 0ull;
+      gathers(q.rb0, mg, q.amv);
+      q.mr = mg;
+    };
+
+    // ---- the flush of a consumed batch: lane = (slot, word), every active word of the slot's
+    // peer into the receiver's packed E row (zeros included: receivers gather by AW mask)
+    auto flush = [&](const GStage& q, int32_t p0, int ns) {
+      for (int s0 = 0; s0 < ns; s0 += SPI) {
+        const int sl = s0 + gl;
+        const bool ok = sl < ns && wvalid;
+        const int o = ok ? L.owner[sl] : 0;
+        const uint32_t wmk = ok ? L.wmask[o] : 0u;
+        const int js = p0 + sl;  // batch slot
+        uint32_t rv = bperm(js & 63, q.rv);
+        int32_t tv = CHURN ? (int32_t)bperm(js & 63, (uint32_t)q.v) : 0;
+        // packed: the sender's active words, in order; else every word of an active sender
+        if (packed ? ((wmk >> wl) & 1u) != 0u : (wmk != 0u && wvalid)) {
+          if (js >= 64) {  // beyond the registers (one peer wider than 64 slots)
+            rv = g.rev[q.rb0 + js];
+            if (CHURN) tv = g.colidx[q.rb0 + js];
+          }
+          uint64_t x = *reinterpret_cast<const uint64_t*>(&L.tbl[sl][wl][0]);
+          if (CHURN && x &&
+              churn_dropped((uint32_t)p.round, gidx(g, u0 + q.b0 + o), gidx(g, tv), p.churn_thr,
+                            p.cseed_lo, p.cseed_hi))
+            x = 0ull;
+          st_row(&Eo[(int64_t)rv * W + (packed ? __popc(wmk & ((1u << wl) - 1u)) : wl)], x);
+          if (x) c[ST_SCATTER] += 1;
+        }
+      }
+    };
+    bool pend = false;  // the last consumed batch's flush is deferred to after the next wait
+    int pend_ns = 0;
+
+    auto consume = [&](GStage& a, GStage& b, GStage& cc, GStage& d) {
+      // 1. arrivals: the first gathers (in flight since the last step) + the rest
+      uint64_t acc = (X[0] | X[1]) | (X[2] | X[3]);
+      const uint64_t need = need_of(a);
+      {
+        uint64_t mg = a.mr;
+        while (__ballot(mg != 0ull)) {
+          gathers(a.rb0, mg, a.amv);
+          acc |= (X[0] | X[1]) | (X[2] | X[3]);
+        }
+        for (int64_t cb = a.rb0 + 64; cb < a.rb1; cb += 64) {  // one peer wider than 64 slots
+          int32_t v = 0;
+          uint32_t aword = 0;
+          uint64_t amv = 0;
+          const bool own = cb + lane < a.rb1 && ((todo >> a.b0) & 1u);
+          if (own) {
+            v = g.colidx[cb + lane];
+            aword = Ap[v >> 5];
+            if (packed) amv = AWp[v];
+          }
+          const uint64_t am = active_slots(a, cb, v, own, aword);
+          const uint64_t ms = my_slots(a, cb);
+          uint64_t m2 = need ? am & ms : 0ull;
+          while (__ballot(m2 != 0ull)) {
+            gathers(cb, m2, amv);
+            acc |= (X[0] | X[1]) | (X[2] | X[3]);
+          }
+        }
+      }
+      // everything loaded so far has landed: say so explicitly, so that no implicit wait on a
+      // younger load (the next batch's gathers) is placed where this batch's data is used
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+      if (pend) {
+        flush(d, 0, pend_ns);
+        pend = false;
+      }
+      // 2. advance the pipeline before this batch's stores and picks
+      first_gathers(b);
+      activity(cc);
+      rows(d);
+      // 3. dedup, frontier row, bitmaps, counters
+      const int n = a.n;
+      const int bi = gl < n ? a.b0 + gl : a.b0;
+      const bool mine = gl < n && ((todo >> bi) & 1u);
+      const int64_t u = u0 + bi;
+      const uint32_t degg = (uint32_t)(readlane64_v(rp, bi + 1) - readlane64_v(rp, bi));
+      const uint64_t nw = acc & need;
+      const uint64_t wm_all = __ballot(nw != 0ull);
+      const uint32_t grp = (uint32_t)((wm_all >> (gl * WP)) & gmask);  // my peer's active words
+      if (nw) st_frow(&st.seen[u * W + wl], a.s | nw);
+      if (mine && grp && wvalid) st_frow(&Fc[u * W + wl], nw);
+      if (nw) {
+        const uint32_t pc = (uint32_t)__popcll(nw);
+        c[ST_NEW] += pc;
+        c[ST_RELAYS] += pc * (degg < (uint32_t)k ? degg : (uint32_t)k);
+        c[ST_ACTIVE_W] += 1;
+        c[ST_WEDGES] += degg;
+      }
+      if (mine && wl == 0 && grp) {
+        if (packed) st.AW[cur][u] = grp;
+        c[ST_ACTIVE_V] += 1;
+        c[ST_DEG_ACT] += degg;
+      }
+      const uint32_t gi = lane < n ? (uint32_t)((wm_all >> (lane * WP)) & gmask) : 0u;
+      aw |= (uint32_t)__ballot(gi != 0u) << a.b0;
+      const uint64_t open = __ballot(mine && wvalid && (a.s | nw) != fm);
+      const bool done_i = lane < n && ((todo >> (a.b0 + lane)) & 1u) && ((open >> (lane * WP)) & gmask) == 0ull;
+      sat |= (uint32_t)__ballot(done_i) << a.b0;
+      if (!wm_all) return;
+      // 4. this round's pushes: picks into the (slot, word) table, then the flush
+      if (lane < n) L.wmask[lane] = gi;
+      const int32_t rel = (int32_t)(rp - a.rb0);
+      if (lane >= a.b0 && lane <= a.b0 + n) L.off[lane - a.b0] = rel;
+      const uint32_t cntb = (uint32_t)__popcll(nw);
+      const uint32_t incl = wave_scan_u32(cntb);
+      const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+      const uint32_t pos0 = incl - cntb;
+      const int32_t nslots = (int32_t)(a.rb1 - a.rb0);
+      const uint32_t gv_base = (uint32_t)(u0 + a.b0);
+      for (int32_t p0 = 0; p0 < nslots; p0 += TS) {
+        const int ns = nslots - p0 < TS ? nslots - p0 : TS;
+        if (lane < ns) {
+          int o = 0;
+          for (int i = 1; i < n; ++i) o += __builtin_amdgcn_readlane(rel, a.b0 + i) <= p0 + lane;
+          L.owner[lane] = (uint8_t)o;
+        }
+        for (int e = lane; e < ns * WP; e += 64) {
+          L.tbl[e >> LW][e & (WP - 1)][0] = 0u;
+          L.tbl[e >> LW][e & (WP - 1)][1] = 0u;
+        }
+        for (uint32_t lb = 0; lb < total; lb += GLIST_G) {
+          const uint32_t ne = total - lb < (uint32_t)GLIST_G ? total - lb : (uint32_t)GLIST_G;
+          uint32_t li = pos0 - lb;
+          for (uint32_t h = (uint32_t)nw; h; h &= h - 1u, ++li)
+            if (li < ne) L.lst[li] = (uint16_t)(((uint32_t)lane << 6) | (uint32_t)__builtin_ctz(h));
+          for (uint32_t h = (uint32_t)(nw >> 32); h; h &= h - 1u, ++li)
+            if (li < ne) L.lst[li] = (uint16_t)(((uint32_t)lane << 6) | 32u | (uint32_t)__builtin_ctz(h));
+          wave_lds_sync();
+          // strided: lane l takes entries l*nbat ..: consecutive entries are one word's bits
+          const uint32_t nbat = (ne + 63) >> 6;
+          const uint32_t i0 = (uint32_t)lane * nbat;
+          const uint32_t my = i0 < ne ? (ne - i0 < nbat ? ne - i0 : nbat) : 0u;
+          for (uint32_t bb = 0; bb < my; ++bb) {
+            const uint32_t e = L.lst[i0 + bb];
+            const uint32_t le = e >> 6, bit = e & 63u;
+            const int gq = (int)(le >> LW), wq = (int)(le & (WP - 1));
+            const int32_t oq = L.off[gq];
+            const uint32_t dq = (uint32_t)(L.off[gq + 1] - oq);
+            const uint32_t mb = 1u << (bit & 31u);
+            uint32_t* const col = &L.tbl[0][wq][bit >> 5];
+            const int32_t base = oq - p0;
+            if (dq <= (uint32_t)k) {  // every connection (node.py:114-120 per target)
+              for (uint32_t q = 0; q < dq; ++q)
+                if ((uint32_t)(base + (int32_t)q) < (uint32_t)ns) atomicOr(col + (base + (int32_t)q) * (WP * 2), mb);
+            } else {
+              uint32_t pk[KK];
+              const uint32_t mg = p.msg_base + (uint32_t)wq * 64u + bit;
+              if constexpr (K > 0)
+                gossip_picks_t<K>((uint32_t)p.round, gidx(g, (int64_t)gv_base + gq), mg, dq, p.gseed_lo,
+                                  p.gseed_hi, pk);
+              else
+                gossip_picks((uint32_t)p.round, gidx(g, (int64_t)gv_base + gq), mg, dq, k, p.gseed_lo,
+                             p.gseed_hi, pk);
+#pragma unroll
+              for (int q = 0; q < KK; ++q) {
+                if (q >= k) break;
+                const int32_t sl = base + (int32_t)pk[q];
+                if ((uint32_t)sl < (uint32_t)ns) atomicOr(col + sl * (WP * 2), mb);
+              }
+            }
+          }
+          wave_lds_sync();
+        }
+        if (nslots <= TS) {  // one window: the flush leaves after the next batch's wait
+          pend = true;
+          pend_ns = ns;
+        } else {
+          flush(a, p0, ns);
+          wave_lds_sync();
+        }
+      }
+    };
+
+    GStage sA, sB, sC, sD;
+    rows(sA);
+    rows(sB);
+    activity(sA);
+    first_gathers(sA);
+    activity(sB);
+    rows(sC);
+    sD.n = 0;
+    // the last consumed batch's deferred flush has no next wait to follow: it leaves here
+    auto last = [&](const GStage& q) {
+      if (pend) flush(q, 0, pend_ns);
+      pend = false;
+    };
+    for (;;) {  // four stages rotate by unrolling (a register copy would wait for its loads)
+      consume(sA, sB, sC, sD);
+      if (sB.n == 0) { last(sA); break; }
+      consume(sB, sC, sD, sA);
+      if (sC.n == 0) { last(sB); break; }
+      consume(sC, sD, sA, sB);
+      if (sD.n == 0) { last(sC); break; }
+      consume(sD, sA, sB, sC);
+      if (sA.n == 0) { last(sD); break; }
+    }
+    wave_lds_sync();
+    if (lane == 0) {
+      st.A[cur][task] = aw;
+      if (sat != sat0) st.S[task] = sat;
+    }
+#pragma unroll
+    for (int q = 0; q < STAT_N; ++q) tot[q] += wave_reduce_u32<false>(c[q]);
+  }
+  if (lane == 0) {
+    unsigned long long* shard = st.stats + (blockIdx.x & (STAT_SHARDS - 1)) * STAT_N;
+#pragma unroll
+    for (int q = 0; q < STAT_N; ++q)
+      if (tot[q]) atomicAdd(shard + q, (unsigned long long)tot[q]);
+  }
+}
+
+template <bool CH, int KT>
+hipError_t launch_lw(int lw, const DevGraph& g, const DevState& st, const RoundParams& p, hipStream_t s) {
+  const int64_t ntasks = (g.V + 31) >> 5;
+#define P2PG_GROUPED(LWV)                                                                    \
+  hipLaunchKernelGGL((k_gossip_fused_grouped<CH, KT, LWV>),                                \
+                     dim3(balanced_grid(k_gossip_fused_grouped<CH, KT, LWV>, ntasks)), dim3(256), \
+                     0, s, g, st, p)
+  switch (lw) {
+    case 0: P2PG_GROUPED(0); break;
+    case 1: P2PG_GROUPED(1); break;
+    case 2: P2PG_GROUPED(2); break;
+    case 3: P2PG_GROUPED(3); break;
+    case 4: P2PG_GROUPED(4); break;
+    default: P2PG_GROUPED(5); break;
+  }
+#undef P2PG_GROUPED
+  return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_gossip_fused_grouped(const DevGraph& g, const DevState& st, const RoundParams& p,
+                                       hipStream_t s) {
+  if (st.W > 32 || st.W < 1) return hipErrorInvalidValue;
+  int lw = 0;
+  while ((1 << lw) < st.W) ++lw;
+  const bool ch = p.churn_thr != 0;
+  if (p.fanout == 3) return ch ? launch_lw<true, 3>(lw, g, st, p, s) : launch_lw<false, 3>(lw, g, st, p, s);
+  return ch ? launch_lw<true, 0>(lw, g, st, p, s) : launch_lw<false, 0>(lw, g, st, p, s);
+}
+
+}  // namespace p2pg

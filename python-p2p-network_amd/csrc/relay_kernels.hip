@@ -24,147 +24,13 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
 #include <type_traits>
 
-#include "internal.h"
-#include "philox.h"
+#include "device_util.h"
 
 namespace p2pg {
 namespace {
-
-constexpr int WPB = 4;  // waves per block (256 threads)
-constexpr int GRID_MAX = 2048;
-
-__device__ __forceinline__ bool bit_test(const uint32_t* bm, int64_t v) {
-  return (bm[v >> 5] >> (v & 31)) & 1u;
-}
-
-__device__ __forceinline__ uint64_t full_mask(int w, int W, int M) {
-  if (w < W - 1 || (M & 63) == 0) return ~0ull;
-  return (1ull << (M & 63)) - 1ull;
-}
-
-__device__ __forceinline__ uint64_t wave_sum(uint64_t x) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
-  return x;
-}
-
-// Wave-wide 32-bit reductions through DPP row shifts and row broadcasts (gfx9 family):
-// four row_shr steps reduce each 16-lane row into its lane 15, row_bcast:15 / row_bcast:31
-// fold the rows into lane 63, which is then read as a scalar.
-template <bool MAX>
-__device__ __forceinline__ uint32_t wave_reduce_u32(uint32_t x) {
-  auto op = [](uint32_t a, uint32_t b) { return MAX ? (a > b ? a : b) : a + b; };
-  x = op(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false));
-  x = op(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false));
-  x = op(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false));
-  x = op(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false));
-  x = op(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false));
-  x = op(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false));
-  return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
-}
-
-// Inclusive prefix sum over the wave (the same DPP steps as wave_reduce_u32<false>).
-__device__ __forceinline__ uint32_t wave_scan_u32(uint32_t x) {
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);
-  return x;
-}
-
-__device__ __forceinline__ void flush_stats(unsigned long long* stats, const uint64_t* c,
-                                            int lane) {
-  unsigned long long* shard = stats + (blockIdx.x & (STAT_SHARDS - 1)) * STAT_N;
-#pragma unroll
-  for (int i = 0; i < STAT_N; ++i) {
-    const uint64_t s = wave_sum(c[i]);
-    if (lane == 0 && s) atomicAdd(shard + i, (unsigned long long)s);
-  }
-}
-
-// Load through the constant address space: a wave-uniform address then becomes a scalar
-// load (s_load, counted on lgkmcnt) instead of a vector load whose vmcnt wait would also wait
-// for every row store the wave still has in flight.  Only for data no kernel writes.
-template <class T>
-__device__ __forceinline__ T ldc(const T* p) {
-  return *(const __attribute__((address_space(4))) T*)p;
-}
-
-// Per-connection E stores of the gossip dense rounds are non-temporal: the planes are re-read
-// a round later, far beyond L2 / MALL reach, and nt stores retire sooner -- which matters
-// because a wave's next gather wait (vmcnt, in order) also waits for its in-flight stores
-// (c4 A/B: fused rounds 267.9 -> 258.7 ms per step).  P2PG_NT_STORE=0 restores plain stores.
-// P2PG_NT_ROWS / P2PG_NT_LOADS extend nt to the fused kernel's seen / frontier row stores and
-// to its E gathers (read once per receiver): together another 260.6 -> 258.7 ms (3 interleaved
-// pairs).
-#ifndef P2PG_NT_STORE
-#define P2PG_NT_STORE 1
-#endif
-#ifndef P2PG_NT_ROWS
-#define P2PG_NT_ROWS 1
-#endif
-#ifndef P2PG_NT_LOADS
-#define P2PG_NT_LOADS 1
-#endif
-#ifndef P2PG_NT_ISSUE
-#define P2PG_NT_ISSUE 0
-#endif
-// streamed-once loads of the fused kernel's row stage (seen word, neighbour ids, receiver slots);
-// nt here measured ±0 (3 interleaved c4 pairs), so off by default
-template <class T>
-__device__ __forceinline__ T ld_once(const T* p) {
-#if P2PG_NT_ISSUE
-  return __builtin_nontemporal_load(p);
-#else
-  return *p;
-#endif
-}
-__device__ __forceinline__ void st_row(uint64_t* p, uint64_t x) {
-#if P2PG_NT_STORE
-  __builtin_nontemporal_store(x, p);
-#else
-  *p = x;
-#endif
-}
-#ifndef P2PG_NT_PULL
-#define P2PG_NT_PULL 1  // c4 update kernel 13.3 -> 12.7 ms per step; c3 flood pull unchanged
-#endif
-// seen / frontier / push-row stores of the pull and update kernels, non-temporal too
-__device__ __forceinline__ void st_prow(uint64_t* p, uint64_t x) {
-#if P2PG_NT_PULL
-  __builtin_nontemporal_store(x, p);
-#else
-  *p = x;
-#endif
-}
-__device__ __forceinline__ void st_frow(uint64_t* p, uint64_t x) {
-#if P2PG_NT_ROWS
-  __builtin_nontemporal_store(x, p);
-#else
-  *p = x;
-#endif
-}
-
-// Global peer id of a local vertex (partitioned runs keep ghosts in global-id order; the
-// Philox keys of churn and gossip are global ids so partitioning cannot change results).
-__device__ __forceinline__ uint32_t gidx(const DevGraph& g, int64_t x) {
-  return g.gid ? (uint32_t)g.gid[x] : (uint32_t)x;
-}
-
-// Same for a wave-uniform vertex: a scalar load (see ldc), no vmcnt wait.
-__device__ __forceinline__ uint32_t gidx_s(const DevGraph& g, int64_t x) {
-  const int64_t xu = __builtin_amdgcn_readfirstlane((int)x);
-  return g.gid ? (uint32_t)ldc(g.gid + xu) : (uint32_t)xu;
-}
-
-// wave index inside the block, forced into an SGPR so task indices stay scalar
-__device__ __forceinline__ int wave_in_block() {
-  return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-}
 
 // ---------------------------------------------------------------------------------------
 // Round 0: origination.  Each message m sets its bit at src[m] in F[0] and seen, and the
@@ -307,11 +173,6 @@ __global__ __launch_bounds__(256) void k_pull(DevGraph g, DevState st, RoundPara
   flush_stats(st.stats, c, lane);
 }
 
-__device__ __forceinline__ int64_t readlane64(int64_t x, int l) {
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, l);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)x >> 32), l);
-  return (int64_t)(((uint64_t)hi << 32) | lo);
-}
 
 // One target's prefetch stage for k_pull1: row range, seen word, first 64 neighbour slots.
 struct PullStage {
@@ -774,11 +635,6 @@ __global__ __launch_bounds__(256) void k_materialize(DevGraph g, DevState st, Ro
   }
 }
 
-// Orders this wave's LDS writes before its later LDS reads by other lanes.
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-}
 
 // Development builds (-DP2PG_PROF): wave clock per fused-kernel segment, summed into st.prof.
 #ifdef P2PG_PROF
@@ -809,16 +665,44 @@ __device__ __forceinline__ void wave_lds_sync() {
 #endif
 
 // LDS of one scatter wave: a GCHUNK x 64-word mask table (two 32-bit halves per word, so
-// 32-bit LDS atomics; the halves adjacent, so a (connection, word) mask is one 64-bit LDS
-// read / write and list entry e = word << 6 | bit addresses its half as u32 index e >> 5) and
-// the compacted list of active (word, bit) entries.
+// 32-bit LDS atomics) and the compacted list of active (word, bit) entries.
+// Half-major rows (P2PG_TBL_HALF_MAJOR, default): connection j's row is [half][word], so the
+// 64 lanes of a pick batch -- entries of ~64 different words -- OR into 64 different banks;
+// with the halves adjacent ([word][half], a 64-bit LDS access per mask) words w and w+32 share
+// a bank (2-way conflicts: 40-49 % of the fused kernel's LDS cycles, profiles/r01/pmc_sq_v11).
+#ifndef P2PG_TBL_HALF_MAJOR
+#define P2PG_TBL_HALF_MAJOR 1
+#endif
 struct ScatterLds {
-  alignas(8) uint32_t tbl[GCHUNK][64][2];
+  alignas(8) uint32_t tbl[GCHUNK * 128];
   uint16_t lst[GLIST];
 };
 
-__device__ __forceinline__ uint64_t& tbl_word(ScatterLds& L, int j, int w) {
-  return *reinterpret_cast<uint64_t*>(&L.tbl[j][w][0]);
+// u32 index of half h of (connection j, word w)
+__device__ __forceinline__ uint32_t tbl_ix(uint32_t j, uint32_t w, uint32_t h) {
+#if P2PG_TBL_HALF_MAJOR
+  return j * 128u + h * 64u + w;
+#else
+  return j * 128u + w * 2u + h;
+#endif
+}
+
+// u32 index of list entry e = word << 6 | bit in connection 0's row
+__device__ __forceinline__ uint32_t tbl_entry_ix(uint32_t e) {
+  return tbl_ix(0u, e >> 6, (e >> 5) & 1u);
+}
+
+__device__ __forceinline__ uint64_t tbl_word(const ScatterLds& L, int j, int w) {
+#if P2PG_TBL_HALF_MAJOR
+  return ((uint64_t)L.tbl[tbl_ix(j, w, 1)] << 32) | L.tbl[tbl_ix(j, w, 0)];
+#else
+  return *reinterpret_cast<const uint64_t*>(&L.tbl[tbl_ix(j, w, 0)]);
+#endif
+}
+
+__device__ __forceinline__ void tbl_clear(ScatterLds& L, int j, int w) {
+  L.tbl[tbl_ix(j, w, 0)] = 0u;
+  L.tbl[tbl_ix(j, w, 1)] = 0u;
 }
 
 // Gossip, round r >= 0: every first receipt (v, m) of round r is pushed to k Philox-chosen
@@ -868,7 +752,7 @@ __device__ __forceinline__ void scatter_row(const DevGraph& g, const DevState& s
     auto one = [&](uint32_t e, bool ok) {
       const uint32_t wl = e >> 6, bit = e & 63u;
       const uint32_t mg = p.msg_base + (uint32_t)((sl * 64 + (int)wl) * 64) + bit;
-      uint32_t* const col = &L.tbl[0][0][0] + (e >> 5);  // = &L.tbl[0][wl][bit >> 5]
+      uint32_t* const col = &L.tbl[tbl_entry_ix(e)];  // connection 0's (word, half)
       const uint32_t mb = ok ? 1u << (bit & 31u) : 0u;
       uint32_t pk[K > 0 ? K : 1];
       gossip_picks_t<(K > 0 ? K : 1)>((uint32_t)p.round, gv, mg, (uint32_t)deg, p.gseed_lo,
@@ -938,15 +822,11 @@ __device__ __forceinline__ void scatter_row(const DevGraph& g, const DevState& s
     if (compact) {
       for (int j0 = 0; j0 < nn; j0 += gper) {
         const int jj = j0 + gl;
-        if (rk && jj < nn) {
-          L.tbl[jj][wc][0] = 0u;
-          L.tbl[jj][wc][1] = 0u;
-        }
+        if (rk && jj < nn) tbl_clear(L, jj, wc);
       }
     } else {
       for (int j = 0; j < nn; ++j) {
-        L.tbl[j][lane][0] = 0u;
-        L.tbl[j][lane][1] = 0u;
+        tbl_clear(L, j, lane);
       }
     }
     // word-major compaction: lane w lists its word's set bits at its exclusive prefix-sum
@@ -978,7 +858,7 @@ __device__ __forceinline__ void scatter_row(const DevGraph& g, const DevState& s
           const uint32_t e = L.lst[i];
           const uint32_t wl = e >> 6, bit = e & 63u;
           const uint32_t mg = p.msg_base + (uint32_t)((sl * 64 + (int)wl) * 64) + bit;
-          uint32_t* const col = &L.tbl[0][wl][bit >> 5];
+          uint32_t* const col = &L.tbl[tbl_ix(0u, wl, bit >> 5)];
           const uint32_t mb = 1u << (bit & 31u);
           uint32_t pk[16];
           gossip_picks((uint32_t)p.round, gv, mg, (uint32_t)deg, k, p.gseed_lo, p.gseed_hi, pk);
@@ -1662,67 +1542,6 @@ __global__ void k_philox(int32_t n, const uint32_t* ctr, uint32_t k0, uint32_t k
   out[4 * i + 3] = r.w;
 }
 
-// Blocks of `kernel` (256 threads) that fit on the whole device at once: a persistent grid of
-// exactly this size has no second, partial wave of blocks (no tail).
-template <class F>
-int resident_blocks(F kernel) {
-  static const void* key[32];
-  static int val[32];
-  static int n = 0;
-  for (int i = 0; i < n; ++i)
-    if (key[i] == (const void*)kernel) return val[i];
-  int nb = 0, dev = 0, cus = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, 256, 0) != hipSuccess || nb < 1) nb = 1;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
-    cus = 256;
-  const int r = nb * cus;
-  if (n < 32) {
-    key[n] = (const void*)kernel;
-    val[n] = r;
-    ++n;
-  }
-  return r;
-}
-
-int grid_tasks_uncapped(int64_t ntasks) {
-  const int64_t b = (ntasks + WPB - 1) / WPB;
-  return (int)(b < 1 ? 1 : (b > 0x7FFFFFFF ? 0x7FFFFFFF : b));
-}
-
-// Grid of a grid-stride task kernel: one 4-wave block per 4 tasks, at most grid_max() blocks
-// (P2PG_GRID_MAX, default GRID_MAX).  Many more blocks than fit at once: a block that drew
-// cheap tasks is replaced by the next one, which evens out the per-wave cost.
-int grid_max() {
-  static const int g = [] {
-    const char* e = std::getenv("P2PG_GRID_MAX");
-    const int v = e ? std::atoi(e) : GRID_MAX;
-    return v > 0 ? v : GRID_MAX;
-  }();
-  return g;
-}
-
-int grid_tasks(int64_t ntasks) {
-  int64_t b = (ntasks + WPB - 1) / WPB;
-  const int64_t cap = grid_max();
-  return (int)(b < 1 ? 1 : (b > cap ? cap : b));
-}
-
-// Grid for the per-peer pull kernels, whose task cost is very uneven (power-law degrees,
-// receipts per peer): P2PG_FUSED_GRID (default 32) x the blocks resident at once, so that
-// blocks finishing early are replaced (measured on config 4: 2x -> 300 ms, 8x -> 267 ms,
-// 32x -> 260 ms for the fused rounds).
-template <class F>
-int balanced_grid(F kernel, int64_t ntasks) {
-  static const int gmul = [] {
-    const char* e = std::getenv("P2PG_FUSED_GRID");
-    const int v = e ? std::atoi(e) : 32;
-    return v > 0 ? v : 32;
-  }();
-  return (int)std::min<int64_t>((int64_t)grid_tasks_uncapped(ntasks),
-                                (int64_t)gmul * resident_blocks(kernel));
-}
-
 }  // namespace
 
 hipError_t launch_zero_rows(uint64_t* plane, int32_t W, const int32_t* rows, int32_t n,
@@ -1826,13 +1645,33 @@ hipError_t launch_gossip_scatter(const DevGraph& g, const DevState& st, const Ro
   return hipGetLastError();
 }
 
+// narrow rows (W <= GROUPED_W_MAX: one rank's share of a message split): several peers per
+// wave.
+// P2PG_GROUPED=0 keeps one wave per peer (A/B only; needs packed rows).
+static bool grouped_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("P2PG_GROUPED");
+    return !(e && std::strcmp(e, "0") == 0);
+  }();
+  return on;
+}
+
+bool gossip_fused_supported(const DevState& st) {
+  if (st.W > 64 || st.E[0] == st.E[1]) return false;
+  return (grouped_enabled() && st.W <= GROUPED_W_MAX) || st.AW[0] != nullptr;
+}
+
 hipError_t launch_gossip_fused(const DevGraph& g, const DevState& st, const RoundParams& p,
                                const HubPlan& hp, const int64_t* big_items, int64_t n_big,
                                hipStream_t s) {
-  if (st.W > 64 || !st.AW[0] || st.E[0] == st.E[1]) return hipErrorInvalidValue;
+  if (!gossip_fused_supported(st)) return hipErrorInvalidValue;
   if (hp.n_items)
     hipLaunchKernelGGL((k_pull_hub_partial<false, true>), dim3(grid_tasks(hp.n_items)),
                        dim3(256), 0, s, g, st, p, hp);
+  if (grouped_enabled() && st.W <= GROUPED_W_MAX) {
+    hipError_t r = launch_gossip_fused_grouped(g, st, p, s);
+    if (r != hipSuccess) return r;
+  } else {
 #define P2PG_FUSED(CH, KK)                                                                   \
   hipLaunchKernelGGL((k_gossip_fused<CH, KK>),                                             \
                      dim3(balanced_grid(k_gossip_fused<CH, KK>, (g.V + 31) >> 5)), dim3(256), 0, \
@@ -1846,6 +1685,7 @@ hipError_t launch_gossip_fused(const DevGraph& g, const DevState& st, const Roun
     default: if (ch) P2PG_FUSED(true, 0); else P2PG_FUSED(false, 0); break;
   }
 #undef P2PG_FUSED
+  }
   if (hp.n_hubs)
     hipLaunchKernelGGL((k_pull_hub_finalize<true>), dim3(grid_tasks(hp.n_hubs)), dim3(256), 0,
                        s, g, st, p, hp);

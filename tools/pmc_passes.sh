@@ -1,7 +1,7 @@
 #!/bin/bash
 # rocprofv3 PMC passes (one counter group per run, per MI355X_MICROARCH.md: FETCH_SIZE and
 # WRITE_SIZE in separate passes) over one broadcast of a workload.
-#   bash tools/pmc_passes.sh c4 gpurun_out/pmc_c4 ["GROUP1" "GROUP2" ...]
+#   [MSGS=512] bash tools/pmc_passes.sh c4 gpurun_out/pmc_c4 ["GROUP1" "GROUP2" ...]
 set -e
 WL=${1:-c4}
 OUT=${2:-gpurun_out/pmc_$WL}
@@ -18,6 +18,6 @@ i=0
 for grp in "${GROUPS_[@]}"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d "$OUT/pass$i" -o p -- \
-      python3 tools/round_profile.py "$WL" 1 > "$OUT/pass$i.log" 2>&1
+      python3 tools/round_profile.py "$WL" 1 $MSGS > "$OUT/pass$i.log" 2>&1
   echo "pass $i ($grp) done"
 done

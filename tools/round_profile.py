@@ -1,6 +1,6 @@
 """Per-round statistics and per-kernel device time of one workload (development aid).
 
-    python tools/round_profile.py c4 > gpurun_out/rounds_c4.json
+    python tools/round_profile.py c4 [runs] [msgs] > gpurun_out/rounds_c4.json
 """
 import json
 import os
@@ -18,7 +18,9 @@ from p2pnetwork.gpu import GraphNetwork, make_sources  # noqa: E402
 def main():
     wl = sys.argv[1] if len(sys.argv) > 1 else "c4"
     runs = int(sys.argv[2]) if len(sys.argv) > 2 else 2
-    w = bench.WORKLOADS[wl]
+    w = dict(bench.WORKLOADS[wl])
+    if len(sys.argv) > 3:
+        w["M"] = int(sys.argv[3])
     g = bench.build_graph(w)
     src = make_sources(g.V, w["M"], seed=1)
     with GraphNetwork(g, mode=w["mode"], fanout=w["fanout"], gossip_seed=0x5EED, timing=True) as net:
@@ -34,6 +36,7 @@ def main():
                 st = net.step()
                 k1 = net.kernel_times()
                 d = st.as_dict()
+                d["push_form"] = st.push_form
                 d["kernel_ms"] = {k: k1[k][0] - k0[k][0] for k in k1}
                 rounds.append(d)
                 if not st.active:
