@@ -160,6 +160,24 @@ int p2pg_set_exchange(p2pg_engine* e, int64_t n_send, const int32_t* send_local,
                       const int32_t* recv_local);
 int p2pg_exchange_pack(p2pg_engine* e, int32_t plane, void* dev_buf);
 int p2pg_exchange_unpack(p2pg_engine* e, int32_t plane, const void* dev_buf);
+/* Compacted exchange: only rows that carry something travel (plane 0: boundary peers with first
+ * receipts this round; plane 1: ghosts that were pushed to), as records of 1 + W int64: the row's
+ * index within the destination's list segment, then its W words.  The lists are cut into one
+ * segment per rank (p2pg_set_exchange_segments: send / recv rows per rank, summing to the
+ * set_exchange lists).  pack_live writes segment q's records from record send_off[q] of dev_buf
+ * (capacity: the list length x (1 + W) int64) and returns the record count per destination in
+ * counts[nseg] (host); unpack_live takes the records of all sources packed in source order and
+ * their counts, and is asynchronous on the engine's stream.                               */
+int p2pg_set_exchange_segments(p2pg_engine* e, int32_t nseg, const int64_t* send_counts,
+                               const int64_t* recv_counts);
+int p2pg_exchange_pack_live(p2pg_engine* e, int32_t plane, void* dev_buf, int64_t* counts);
+int p2pg_exchange_unpack_live(p2pg_engine* e, int32_t plane, const void* dev_buf, const int64_t* counts);
+/* A round in two calls, so a vertex-partitioned rank overlaps the exchange of the last round's
+ * rows with work: step_begin launches the pull / update of the peers with no ghost neighbour
+ * (they need none of the exchanged rows) and returns at once; step_end runs the rest of the
+ * round once the rows are unpacked (= p2pg_step).  p2pg_step alone does both.              */
+int p2pg_step_begin(p2pg_engine* e);
+int p2pg_step_end(p2pg_engine* e, p2pg_round_stats* out);
 /* ---- dynamic topology --------------------------------------------
  * Connection changes between rounds: n_add pairs to connect (Node.connect_with_node,
  * node.py:122-176) and n_del pairs to disconnect (Node.disconnect_with_node, node.py:178-189,

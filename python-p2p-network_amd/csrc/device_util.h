@@ -143,6 +143,15 @@ __device__ __forceinline__ uint32_t gidx_s(const DevGraph& g, int64_t x) {
   return g.gid ? (uint32_t)ldc(g.gid + xu) : (uint32_t)xu;
 }
 
+// The activity word of a task at the end of a (phase of a) round: a phase-1 pass adds its
+// peers' bits to those of phase 0; a whole-round or phase-0 pass writes the word.
+__device__ __forceinline__ void put_active(uint32_t* A, int64_t task, uint32_t aw, const RoundParams& p) {
+  if (p.phase == 1)
+    A[task] |= aw;
+  else
+    A[task] = aw;
+}
+
 // wave index inside the block, forced into an SGPR so task indices stay scalar
 __device__ __forceinline__ int wave_in_block() {
   return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));

@@ -58,6 +58,13 @@ struct p2pg_engine {
   int32_t* d_send = nullptr;
   int32_t* d_recv = nullptr;
   int64_t n_send = 0, n_recv = 0;
+  uint32_t* d_border = nullptr;       // owned peers with a ghost neighbour (phase 1 of a round)
+  std::vector<int64_t> send_seg, recv_seg;  // list offsets per rank (p2pg_set_exchange_segments)
+  int64_t* d_send_seg = nullptr;
+  int64_t* d_recv_seg = nullptr;
+  unsigned long long* d_seg_cnt = nullptr;  // live rows per destination (pack_live)
+  unsigned long long* h_seg_cnt = nullptr;  // pinned
+  bool begun = false;                 // p2pg_step_begin ran this round's phase 0
   bool last_push_e = false;    // gossip: pushes of the previous round went to E (dense)
   double e_thresh = 0.04;      // store-mode when active words >= thresh * active rows * W
                                // (c4 A/B, interleaved runs: 0.04 320.4 ms vs 0.1 324.3 ms)
@@ -184,6 +191,14 @@ void free_graph(p2pg_engine* e) {
   dfree(e->d_gid);
   dfree(e->d_send);
   dfree(e->d_recv);
+  dfree(e->d_border);
+  dfree(e->d_send_seg);
+  dfree(e->d_recv_seg);
+  dfree(e->d_seg_cnt);
+  if (e->h_seg_cnt) (void)hipHostFree(e->h_seg_cnt);
+  e->h_seg_cnt = nullptr;
+  e->send_seg.clear();
+  e->recv_seg.clear();
   e->h_gid.clear();
   e->n_send = e->n_recv = 0;
   e->hp = HubPlan{};
@@ -202,6 +217,8 @@ RoundParams params(const p2pg_engine* e) {
   p.churn_thr = e->cfg.churn_threshold;
   p.cseed_lo = (uint32_t)e->cfg.churn_seed;
   p.cseed_hi = (uint32_t)(e->cfg.churn_seed >> 32);
+  p.border = nullptr;
+  p.phase = -1;
   return p;
 }
 
@@ -537,6 +554,7 @@ int p2pg_reset(p2pg_engine* e) {
   }
   e->round = 0;
   e->done = false;
+  e->begun = false;
   e->last_push_e = false;
   e->consume_next = false;
   e->total_relays = 0;
@@ -549,23 +567,63 @@ int p2pg_reset(p2pg_engine* e) {
   return P2PG_OK;
 }
 
+}  // extern "C"
+
+namespace {
+
+// Can this round's pull / update run in two phases (interior peers, then border peers)?
+// Vertex-partitioned ranks with ghosts, rounds r >= 1 of the flood pull or the gossip update.
+bool split_round(const p2pg_engine* e) {
+  return e->d_border && e->round > 0 && !e->consume_next &&
+         (e->cfg.mode == P2PG_MODE_FLOOD || !e->last_push_e);
+}
+
+}  // namespace
+
+extern "C" {
+
+int p2pg_step_begin(p2pg_engine* e) {
+  if (!e || !e->have_state) return fail(e, P2PG_ERR_STATE, "step_begin: no sources set");
+  if (e->begun) return fail(e, P2PG_ERR_STATE, "step_begin: the round has begun already");
+  if (e->done) return P2PG_OK;
+  HIPCHK(e, hipSetDevice(e->cfg.device));
+  DevState& s = e->st;
+  HIPCHK(e, hipMemsetAsync(s.stats, 0, sizeof(unsigned long long) * STAT_N * STAT_SHARDS, e->stream));
+  e->begun = true;
+  if (!split_round(e)) return P2PG_OK;
+  // phase 0: peers without a ghost neighbour, which need none of the rows still in transit
+  const DevGraph g = graph(e);
+  RoundParams p = params(e);
+  p.border = e->d_border;
+  p.phase = 0;
+  if (e->cfg.mode == P2PG_MODE_FLOOD)
+    return timed(e, 1, [&] { return launch_flood_pull(g, s, p, e->hp, e->stream); });
+  return timed(e, 4, [&] { return launch_gossip_update(g, s, p, e->stream); });
+}
+
 int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
   if (!e || !e->have_state) return fail(e, P2PG_ERR_STATE, "step: no sources set");
   if (e->done) {
+    e->begun = false;
     if (out) {
       std::memset(out, 0, sizeof(*out));
       out->round = e->round;
     }
     return 0;
   }
+  int rc;
+  if (!e->begun && (rc = p2pg_step_begin(e))) return rc;
   HIPCHK(e, hipSetDevice(e->cfg.device));
   DevState& s = e->st;
   if (e->arr_round >= 0 && e->round > e->arr_round) free_arr(e);
   const DevGraph g = graph(e);
-  const RoundParams p = params(e);
+  RoundParams p = params(e);
+  if (split_round(e)) {  // phase 0 ran in step_begin: the border peers now
+    p.border = e->d_border;
+    p.phase = 1;
+  }
+  e->begun = false;
   const bool gossip = e->cfg.mode == P2PG_MODE_GOSSIP;
-  HIPCHK(e, hipMemsetAsync(s.stats, 0, sizeof(unsigned long long) * STAT_N * STAT_SHARDS, e->stream));
-  int rc;
   bool fused_round = false;
   uint64_t host_new = 0, host_relays = 0, host_av = 0, host_aw = 0, host_wedge = 0, host_degact = 0;
   if (e->round == 0) {
@@ -703,6 +761,8 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
   return active ? 1 : 0;
 }
 
+int p2pg_step_end(p2pg_engine* e, p2pg_round_stats* out) { return p2pg_step(e, out); }
+
 int p2pg_run(p2pg_engine* e, int32_t max_rounds, p2pg_round_stats* per_round,
              int32_t* n_rounds) {
   if (!e) return P2PG_ERR_ARG;
@@ -838,6 +898,100 @@ int p2pg_set_exchange(p2pg_engine* e, int64_t n_send, const int32_t* send_local,
   HIPCHK(e, hipMalloc((void**)&e->d_recv, sizeof(int32_t) * (n_recv ? n_recv : 1)));
   if (n_send) HIPCHK(e, hipMemcpy(e->d_send, send_local, sizeof(int32_t) * n_send, hipMemcpyHostToDevice));
   if (n_recv) HIPCHK(e, hipMemcpy(e->d_recv, recv_local, sizeof(int32_t) * n_recv, hipMemcpyHostToDevice));
+  // border peers: a ghost (recv list) among the neighbours -- their pull / update waits for the
+  // exchanged rows (phase 1); every other peer can run while the exchange is in flight
+  dfree(e->d_border);
+  if (n_recv) {
+    std::vector<uint8_t> ghost((size_t)e->V, 0);
+    for (int64_t i = 0; i < n_recv; ++i) ghost[recv_local[i]] = 1;
+    std::vector<uint32_t> border((size_t)((e->V + 31) / 32), 0u);
+    for (int64_t v = 0; v < e->V; ++v)
+      for (int64_t j = e->h_rowptr[v]; j < e->h_rowptr[v + 1]; ++j)
+        if (ghost[e->h_colidx[j]]) {
+          border[v >> 5] |= 1u << (v & 31);
+          break;
+        }
+    HIPCHK(e, hipMalloc((void**)&e->d_border, sizeof(uint32_t) * border.size()));
+    HIPCHK(e, hipMemcpy(e->d_border, border.data(), sizeof(uint32_t) * border.size(), hipMemcpyHostToDevice));
+  }
+  return P2PG_OK;
+}
+
+int p2pg_set_exchange_segments(p2pg_engine* e, int32_t nseg, const int64_t* send_counts,
+                               const int64_t* recv_counts) {
+  if (!e || !e->d_send || nseg < 1 || nseg > P2PG_MAX_RANKS || !send_counts || !recv_counts)
+    return fail(e, P2PG_ERR_ARG, "set_exchange_segments: bad arguments (set_exchange first; 1..16 ranks)");
+  std::vector<int64_t> so(nseg + 1, 0), ro(nseg + 1, 0);
+  for (int q = 0; q < nseg; ++q) {
+    if (send_counts[q] < 0 || recv_counts[q] < 0) return fail(e, P2PG_ERR_ARG, "set_exchange_segments: negative count");
+    so[q + 1] = so[q] + send_counts[q];
+    ro[q + 1] = ro[q] + recv_counts[q];
+  }
+  if (so[nseg] != e->n_send || ro[nseg] != e->n_recv)
+    return fail(e, P2PG_ERR_ARG, "set_exchange_segments: counts do not add up to the exchange lists");
+  HIPCHK(e, hipSetDevice(e->cfg.device));
+  dfree(e->d_send_seg);
+  dfree(e->d_recv_seg);
+  dfree(e->d_seg_cnt);
+  if (e->h_seg_cnt) (void)hipHostFree(e->h_seg_cnt);
+  e->h_seg_cnt = nullptr;
+  e->send_seg = so;
+  e->recv_seg = ro;
+  HIPCHK(e, hipMalloc((void**)&e->d_send_seg, sizeof(int64_t) * so.size()));
+  HIPCHK(e, hipMalloc((void**)&e->d_recv_seg, sizeof(int64_t) * ro.size()));
+  HIPCHK(e, hipMemcpy(e->d_send_seg, so.data(), sizeof(int64_t) * so.size(), hipMemcpyHostToDevice));
+  HIPCHK(e, hipMemcpy(e->d_recv_seg, ro.data(), sizeof(int64_t) * ro.size(), hipMemcpyHostToDevice));
+  HIPCHK(e, hipMalloc((void**)&e->d_seg_cnt, sizeof(unsigned long long) * P2PG_MAX_RANKS));
+  HIPCHK(e, hipHostMalloc((void**)&e->h_seg_cnt, sizeof(unsigned long long) * P2PG_MAX_RANKS));
+  return P2PG_OK;
+}
+
+int p2pg_exchange_pack_live(p2pg_engine* e, int32_t plane, void* dev_buf, int64_t* counts) {
+  if (!e || !e->have_state || e->round == 0 || (plane != 0 && plane != 1) || !dev_buf || !counts)
+    return fail(e, P2PG_ERR_STATE, "exchange_pack_live: need a completed round, plane 0 or 1, buffers");
+  if (!e->d_seg_cnt) return fail(e, P2PG_ERR_STATE, "exchange_pack_live: set_exchange_segments first");
+  if (plane == 1 && e->cfg.mode != P2PG_MODE_GOSSIP)
+    return fail(e, P2PG_ERR_ARG, "exchange_pack_live: plane 1 is for gossip pushes");
+  HIPCHK(e, hipSetDevice(e->cfg.device));
+  const int nseg = (int)e->send_seg.size() - 1;
+  // plane 0 moves frontier rows owner -> ghost (send list); plane 1 pushes ghost -> owner
+  const bool fwd = plane == 0;
+  const int32_t* ids = fwd ? e->d_send : e->d_recv;
+  const int64_t n = fwd ? e->n_send : e->n_recv;
+  const int64_t* seg = fwd ? e->d_send_seg : e->d_recv_seg;
+  HIPCHK(e, hipMemsetAsync(e->d_seg_cnt, 0, sizeof(unsigned long long) * P2PG_MAX_RANKS, e->stream));
+  hipError_t r = launch_pack_live(e->st, plane, e->round - 1, ids, n, seg, nseg, e->d_seg_cnt,
+                                  (int64_t*)dev_buf, e->stream);
+  if (r == hipSuccess)
+    r = hipMemcpyAsync(e->h_seg_cnt, e->d_seg_cnt, sizeof(unsigned long long) * nseg, hipMemcpyDeviceToHost,
+                       e->stream);
+  if (r == hipSuccess) r = hipStreamSynchronize(e->stream);
+  if (r != hipSuccess) return fail(e, P2PG_ERR_HIP, std::string("exchange_pack_live: ") + hipGetErrorString(r));
+  for (int q = 0; q < nseg; ++q) counts[q] = (int64_t)e->h_seg_cnt[q];
+  return P2PG_OK;
+}
+
+int p2pg_exchange_unpack_live(p2pg_engine* e, int32_t plane, const void* dev_buf, const int64_t* counts) {
+  if (!e || !e->have_state || e->round == 0 || (plane != 0 && plane != 1) || !counts)
+    return fail(e, P2PG_ERR_STATE, "exchange_unpack_live: need a completed round, plane 0 or 1, counts");
+  if (!e->d_seg_cnt) return fail(e, P2PG_ERR_STATE, "exchange_unpack_live: set_exchange_segments first");
+  HIPCHK(e, hipSetDevice(e->cfg.device));
+  const int nseg = (int)e->send_seg.size() - 1;
+  const bool fwd = plane == 0;  // plane 0 lands in the recv list (ghosts), plane 1 in the send list
+  const int32_t* ids = fwd ? e->d_recv : e->d_send;
+  const std::vector<int64_t>& lst = fwd ? e->recv_seg : e->send_seg;
+  const int64_t* lseg = fwd ? e->d_recv_seg : e->d_send_seg;
+  int64_t ro[P2PG_MAX_RANKS + 1] = {0};
+  for (int q = 0; q < nseg; ++q) {
+    if (counts[q] < 0 || counts[q] > lst[q + 1] - lst[q])
+      return fail(e, P2PG_ERR_ARG, "exchange_unpack_live: more records than the list segment holds");
+    ro[q + 1] = ro[q] + counts[q];
+  }
+  if (ro[nseg] > 0 && !dev_buf) return fail(e, P2PG_ERR_ARG, "exchange_unpack_live: no buffer");
+  // asynchronous on the engine stream: the next step orders after it
+  hipError_t r = launch_unpack_live(e->st, plane, e->round - 1, ids, lseg, nseg, ro, (const int64_t*)dev_buf,
+                                    e->stream);
+  if (r != hipSuccess) return fail(e, P2PG_ERR_HIP, std::string("exchange_unpack_live: ") + hipGetErrorString(r));
   return P2PG_OK;
 }
 

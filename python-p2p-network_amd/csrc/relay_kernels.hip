@@ -84,7 +84,7 @@ __global__ __launch_bounds__(256) void k_pull(DevGraph g, DevState st, RoundPara
     const int64_t u0 = task << 5;
     const uint32_t sat0 = st.S[task];
     uint32_t sat = sat0;
-    uint32_t todo = ~sat0;
+    uint32_t todo = ~sat0 & phase_mask(p, task);
     if (V - u0 < 32) todo &= (1u << (V - u0)) - 1u;
     uint32_t aw = 0;
     while (todo) {
@@ -166,7 +166,7 @@ __global__ __launch_bounds__(256) void k_pull(DevGraph g, DevState st, RoundPara
       if (row_full) sat |= 1u << b;
     }
     if (lane == 0) {
-      st.A[cur][task] = aw;
+      put_active(st.A[cur], task, aw, p);
       if (sat != sat0) st.S[task] = sat;
     }
   }
@@ -249,11 +249,11 @@ __global__ __launch_bounds__(256, P2PG_PULL_WAVES) void k_pull1(DevGraph g, DevS
        task += (int64_t)gridDim.x * WPB) {
     const int64_t u0 = task << 5;
     const uint32_t sat0 = st.S[task];
-    uint32_t todo = ~sat0;
+    uint32_t todo = ~sat0 & phase_mask(p, task);
     if (g.H) todo &= ~g.H[task];  // hubs: k_pull_hub_* items
     if (V - u0 < 32) todo &= (1u << (V - u0)) - 1u;
     if (!todo) {
-      if (lane == 0) st.A[cur][task] = 0u;
+      if (lane == 0 && p.phase != 1) st.A[cur][task] = 0u;
       continue;
     }
     int64_t rp = 0;
@@ -392,7 +392,7 @@ __global__ __launch_bounds__(256, P2PG_PULL_WAVES) void k_pull1(DevGraph g, DevS
       s2 = s3;
     }
     if (lane == 0) {
-      st.A[cur][task] = aw;
+      put_active(st.A[cur], task, aw, p);
       if (sat != sat0) st.S[task] = sat;
     }
   }
@@ -536,9 +536,10 @@ __global__ __launch_bounds__(256) void k_gossip_update(DevGraph g, DevState st,
 
   for (int64_t task = (int64_t)blockIdx.x * WPB + wib; task < ntasks;
        task += (int64_t)gridDim.x * WPB) {
-    uint32_t tw = st.T[cur][task];
+    const uint32_t tw0 = st.T[cur][task];
+    uint32_t tw = tw0 & phase_mask(p, task);
     uint32_t aw = 0;
-    if (tw && lane == 0) st.T[cur][task] = 0u;
+    if (tw && lane == 0) st.T[cur][task] = tw0 & ~tw;  // consumed (the other phase's bits stay)
     while (tw) {
       const int b = __builtin_ctz(tw);
       tw &= tw - 1u;
@@ -584,7 +585,7 @@ __global__ __launch_bounds__(256) void k_gossip_update(DevGraph g, DevState st,
         }
       }
     }
-    if (lane == 0) st.A[cur][task] = aw;
+    if (lane == 0) put_active(st.A[cur], task, aw, p);
   }
   flush_stats(st.stats, c, lane);
 }
@@ -1523,6 +1524,91 @@ __global__ __launch_bounds__(256) void k_unpack(DevState st, int plane, int roun
   }
 }
 
+// Compacted exchange (vertex-partitioned runs): only live rows travel, as records
+// [index in the destination's list segment][W words].  plane 0: frontier rows of round `round`
+// (live = A bit) of the send list; plane 1: gossip pushes pending for round+1 in ghost rows
+// (live = T bit; row and bit are cleared here).  One wave per 64 list entries (lane = entry)
+// computes liveness and destination segment, reserves record slots with one atomic per
+// (wave, segment), then copies each live row with lane = word.
+__global__ __launch_bounds__(256) void k_pack_live(DevState st, int plane, int round,
+                                                   const int32_t* __restrict__ ids, int64_t n,
+                                                   const int64_t* __restrict__ seg_off, int nseg,
+                                                   unsigned long long* __restrict__ seg_cnt,
+                                                   int64_t* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int W = st.W;
+  const int64_t R = 1 + W;  // int64 per record
+  const int64_t nwaves = (int64_t)gridDim.x * WPB;
+  uint64_t* __restrict__ src = plane == 0 ? st.F[round & 1] : st.next[(round + 1) & 1];
+  uint32_t* __restrict__ bits = plane == 0 ? st.A[round & 1] : st.T[(round + 1) & 1];
+  for (int64_t base = ((int64_t)blockIdx.x * WPB + wave_in_block()) * 64; base < n; base += nwaves * 64) {
+    const int64_t i = base + lane;
+    const bool valid = i < n;
+    const int64_t v = valid ? ids[i] : 0;
+    const bool live = valid && bit_test(bits, v);
+    int seg = 0;
+    for (int q = 1; q < nseg; ++q) seg += i >= ldc(seg_off + q);
+    int64_t pos = 0;  // record slot within the segment
+    uint64_t todo = __ballot(live);
+    while (todo) {
+      const int q0 = __builtin_amdgcn_readlane(seg, __builtin_ctzll(todo));
+      const uint64_t m = __ballot(live && seg == q0);
+      unsigned long long b0 = 0;
+      if (lane == 0) b0 = atomicAdd(&seg_cnt[q0], (unsigned long long)__popcll(m));
+      b0 = (unsigned long long)readlane64((int64_t)b0, 0);
+      if (live && seg == q0)
+        pos = (int64_t)b0 + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      todo &= ~m;
+    }
+    uint64_t lv = __ballot(live);
+    while (lv) {
+      const int l = __builtin_ctzll(lv);
+      lv &= lv - 1ull;
+      const int64_t vl = readlane64(v, l);
+      const int sq = __builtin_amdgcn_readlane(seg, l);
+      const int64_t rec = (ldc(seg_off + sq) + readlane64(pos, l)) * R;
+      if (lane == 0) out[rec] = readlane64(i, l) - ldc(seg_off + sq);
+      for (int w = lane; w < W; w += 64) {
+        out[rec + 1 + w] = (int64_t)src[vl * W + w];
+        if (plane == 1) src[vl * W + w] = 0ull;
+      }
+      if (plane == 1 && lane == 0) atomicAnd(&bits[vl >> 5], ~(1u << (vl & 31)));
+    }
+  }
+}
+
+// The receiving side: record i came from source rank p with rec_off[p] <= i < rec_off[p+1];
+// its index selects the peer in that rank's segment of the list (plane 0: ghosts by owner,
+// rows stored + A bit; plane 1: owned boundary peers by neighbour rank, rows ORed + T bit).
+struct RecOffsets {
+  int64_t off[P2PG_MAX_RANKS + 1];
+};
+
+__global__ __launch_bounds__(256) void k_unpack_live(DevState st, int plane, int round,
+                                                     const int32_t* __restrict__ ids,
+                                                     const int64_t* __restrict__ list_off, int nseg,
+                                                     RecOffsets ro, const int64_t* __restrict__ in) {
+  const int lane = threadIdx.x & 63;
+  const int W = st.W;
+  const int64_t R = 1 + W;
+  const int64_t nrec = ro.off[nseg];
+  for (int64_t i = (int64_t)blockIdx.x * WPB + wave_in_block(); i < nrec; i += (int64_t)gridDim.x * WPB) {
+    int p = 0;
+    for (int q = 1; q < nseg; ++q) p += i >= ro.off[q];
+    const int64_t idx = ldc(in + i * R);
+    const int64_t v = ids[ldc(list_off + p) + idx];
+    for (int w = lane; w < W; w += 64) {
+      const uint64_t x = (uint64_t)in[i * R + 1 + w];
+      if (plane == 0) st.F[round & 1][v * W + w] = x;
+      else if (x) atomicOr((unsigned long long*)&st.next[(round + 1) & 1][v * W + w], (unsigned long long)x);
+    }
+    if (lane == 0) {
+      if (plane == 0) atomicOr(&st.A[round & 1][v >> 5], 1u << (v & 31));
+      else atomicOr(&st.T[(round + 1) & 1][v >> 5], 1u << (v & 31));
+    }
+  }
+}
+
 __global__ void k_column(const uint64_t* __restrict__ plane, int32_t W, int32_t w, int64_t V,
                          uint64_t* __restrict__ out) {
   for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < V;
@@ -1564,13 +1650,14 @@ hipError_t pull_with_hubs(const DevGraph& g, const DevState& st, const RoundPara
                           const HubPlan& hp, hipStream_t s) {
   const int grid = grid_tasks((g.V + 31) >> 5);
   if (st.W <= 64) {
-    if (hp.n_items)
+    // hubs (deg > HUB_T) are pulled whole in the last phase of a round (phase -1 or 1)
+    if (hp.n_items && p.phase != 0)
       hipLaunchKernelGGL((k_pull_hub_partial<CHURN, GOSSIP>), dim3(grid_tasks(hp.n_items)),
                          dim3(256), 0, s, g, st, p, hp);
     hipLaunchKernelGGL((k_pull1<CHURN, GOSSIP>),
                        dim3(balanced_grid(k_pull1<CHURN, GOSSIP>, (g.V + 31) >> 5)), dim3(256), 0,
                        s, g, st, p);
-    if (hp.n_hubs)
+    if (hp.n_hubs && p.phase != 0)
       hipLaunchKernelGGL((k_pull_hub_finalize<GOSSIP>), dim3(grid_tasks(hp.n_hubs)), dim3(256),
                          0, s, g, st, p, hp);
   } else {
@@ -1723,6 +1810,28 @@ hipError_t launch_unpack(const DevState& st, int plane, int round, const int32_t
                          const uint64_t* in, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_unpack, dim3(grid_tasks(n)), dim3(256), 0, s, st, plane, round, ids, n, in);
+  return hipGetLastError();
+}
+
+hipError_t launch_pack_live(const DevState& st, int plane, int round, const int32_t* ids, int64_t n,
+                            const int64_t* seg_off, int nseg, unsigned long long* seg_cnt,
+                            int64_t* out, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const int64_t waves = (n + 63) / 64;
+  hipLaunchKernelGGL(k_pack_live, dim3(grid_tasks(waves)), dim3(256), 0, s, st, plane, round, ids, n,
+                     seg_off, nseg, seg_cnt, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_unpack_live(const DevState& st, int plane, int round, const int32_t* ids,
+                              const int64_t* list_off, int nseg, const int64_t* rec_off,
+                              const int64_t* in, hipStream_t s) {
+  if (nseg < 1 || nseg > P2PG_MAX_RANKS) return hipErrorInvalidValue;
+  RecOffsets ro{};
+  for (int q = 0; q <= nseg; ++q) ro.off[q] = rec_off[q];
+  if (ro.off[nseg] <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_unpack_live, dim3(grid_tasks(ro.off[nseg])), dim3(256), 0, s, st, plane, round,
+                     ids, list_off, nseg, ro, in);
   return hipGetLastError();
 }
 

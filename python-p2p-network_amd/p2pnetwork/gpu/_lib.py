@@ -95,6 +95,11 @@ SIGNATURES = {
     "p2pg_set_exchange": (ctypes.c_int, [_P, _I64, _P, _I64, _P]),
     "p2pg_exchange_pack": (ctypes.c_int, [_P, _I32, _P]),
     "p2pg_exchange_unpack": (ctypes.c_int, [_P, _I32, _P]),
+    "p2pg_set_exchange_segments": (ctypes.c_int, [_P, _I32, _P, _P]),
+    "p2pg_exchange_pack_live": (ctypes.c_int, [_P, _I32, _P, _P]),
+    "p2pg_exchange_unpack_live": (ctypes.c_int, [_P, _I32, _P, _P]),
+    "p2pg_step_begin": (ctypes.c_int, [_P]),
+    "p2pg_step_end": (ctypes.c_int, [_P, ctypes.POINTER(RoundStatsC)]),
     "p2pg_set_stream": (ctypes.c_int, [_P, _P]),
     "p2pg_device_philox": (ctypes.c_int, [_P, _I32, _P, _P, _P]),
     "p2pg_update_edges": (ctypes.c_int, [_P, _I64, _P, _I64, _P]),

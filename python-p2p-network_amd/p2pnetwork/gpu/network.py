@@ -167,6 +167,14 @@ class GraphNetwork:
         self.rounds = []
         self.message_count_send = 0
 
+    def step_begin(self):
+        """Start the next round asynchronously: on a vertex-partitioned rank, the peers with no
+        ghost neighbour (p2pg_step_begin); ``step`` / ``step_end`` finishes the round."""
+        self._check(_lib.lib().p2pg_step_begin(self._h))
+
+    def step_end(self):
+        return self.step()
+
     def step(self):
         """Run one round; returns its RoundStats (``active`` = messages still in flight)."""
         s = _lib.RoundStatsC()
@@ -318,6 +326,26 @@ class GraphNetwork:
         s = np.ascontiguousarray(send_local, dtype=np.int32)
         r = np.ascontiguousarray(recv_local, dtype=np.int32)
         self._check(_lib.lib().p2pg_set_exchange(self._h, len(s), _lib.ptr(s), len(r), _lib.ptr(r)))
+
+    def set_exchange_segments(self, send_counts, recv_counts):
+        """Rows per rank of the send / recv lists (p2pg_set_exchange_segments)."""
+        sc = np.ascontiguousarray(send_counts, dtype=np.int64)
+        rc = np.ascontiguousarray(recv_counts, dtype=np.int64)
+        self._nseg = len(sc)
+        self._check(_lib.lib().p2pg_set_exchange_segments(self._h, len(sc), _lib.ptr(sc), _lib.ptr(rc)))
+
+    def exchange_pack_live(self, plane, buf):
+        """Pack the live rows of the last round as records into device buffer ``buf``; returns
+        the record count per destination rank (p2pg_exchange_pack_live)."""
+        counts = np.zeros(self._nseg, dtype=np.int64)
+        self._check(_lib.lib().p2pg_exchange_pack_live(self._h, int(plane), ctypes.c_void_p(buf.data_ptr()),
+                                                       _lib.ptr(counts)))
+        return counts
+
+    def exchange_unpack_live(self, plane, buf, counts):
+        c = np.ascontiguousarray(counts, dtype=np.int64)
+        self._check(_lib.lib().p2pg_exchange_unpack_live(self._h, int(plane), ctypes.c_void_p(buf.data_ptr()),
+                                                         _lib.ptr(c)))
 
     def alloc_exchange(self, n_words):
         """Device buffer for exchange rows (a torch tensor on this engine's GPU)."""

@@ -11,6 +11,9 @@ tests):
   next round's pull reads them like local rows;
 * gossip: pushes addressed to ghosts go ghost -> owner, ORed into the owner's push rows.
 
+Only rows that carry something travel (records packed on the device), and the peers without a
+ghost neighbour run the next round while the records are in flight.
+
 Local ids follow global id order (ghosts interleaved), so every ascending-id rule (the
 lowest-id sender tie-break, gossip's sorted candidate list) is the same as on one GPU, and the
 Philox keys of gossip and churn use global ids: results are bit-identical to a single-engine
@@ -91,100 +94,82 @@ class VertexPartition:
         return np.where(held, pos, self.dummy).astype(np.int32)
 
 
-def live_rows(send, send_counts, W):
-    """Compaction of an exchange buffer: (mask, rows, counts) = a uint8 flag per row (row has a
-    non-zero word), the live rows in order, and the live-row count per destination segment.
-    Dead rows carry nothing: a flood row of an inactive boundary peer (the receiver's pull has
-    already cleared the ghost's activity bit for the round) or a gossip ghost nobody pushed to."""
-    import torch
-    n = int(np.sum(send_counts))
-    rows = send[:n * W].view(n, W)
-    live = (rows != 0).any(dim=1)
-    bounds = np.concatenate([[0], np.cumsum(send_counts)]).astype(np.int64)
-    per = [live[int(a):int(b)].sum() for a, b in zip(bounds[:-1], bounds[1:])]
-    counts = torch.stack(per).cpu().numpy().astype(np.int64) if per else np.zeros(0, np.int64)
-    return live.to(torch.uint8), rows[live].reshape(-1), counts
-
-
-def expand_rows(mask, rows, W):
-    """Inverse of live_rows on the receiving side: full rows, zeros where the flag is 0."""
-    import torch
-    full = torch.zeros((mask.numel(), W), dtype=rows.dtype, device=rows.device)
-    full[mask.to(torch.bool)] = rows.view(-1, W)
-    return full.view(-1)
-
-
 class TorchTransport:
-    """All-to-all and sum-reduce over a torch.distributed process group.  With the nccl
-    backend (RCCL on ROCm) the rows move device-to-device over xGMI; with gloo they are
-    staged through host memory (CPU tests, or two ranks sharing one GPU).
+    """The two collectives of a partitioned round over a torch.distributed process group.
+    With the nccl backend (RCCL on ROCm) records move device-to-device over xGMI; with gloo
+    they are staged through host memory (CPU tests, or ranks sharing one GPU).
 
-    Rows go compacted (``sparse``, default): one byte per boundary row says whether the row
-    travels, and only rows with a non-zero word do -- outside the peak rounds most boundary
-    peers are inactive, and the all-to-all moves 512 B per row otherwise."""
+    * ``exchange_counts(vec)``: all-gather of one small int64 vector per rank (each rank's
+      record count per destination + its round counters) -> [world, len];
+    * ``exchange_records(...)``: grouped point-to-point sends / receives of the packed records
+      (``batch_isend_irecv``), exactly the live rows each peer rank needs."""
 
-    def __init__(self, device=None, group=None, sparse=True):
+    def __init__(self, device=None, group=None):
         import torch
         import torch.distributed as dist
         self.torch, self.dist, self.group = torch, dist, group
         self.backend = dist.get_backend(group)
         self.device = device
-        self.sparse = sparse
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
         self.rows_total = 0  # boundary rows offered / actually sent (exchange volume)
         self.rows_sent = 0
 
-    def _a2a(self, recv, send, outs, ins):
-        torch, dist = self.torch, self.dist
-        if self.backend == "nccl":
-            dist.all_to_all_single(recv, send, outs, ins, group=self.group)
-            torch.cuda.synchronize(send.device)
-            return recv
-        r = recv.cpu()
-        dist.all_to_all_single(r, send.cpu(), outs, ins, group=self.group)
-        return r.to(send.device)
-
-    def alltoall_rows(self, send, send_counts, recv_counts, W):
-        """send: tensor [sum(send_counts) * W] int64 (on self.device); returns the recv tensor
-        (full rows, in the receiver's list order)."""
-        torch = self.torch
-        n_out, n_in = int(sum(send_counts)), int(sum(recv_counts))
-        self.rows_total += n_out
-        if not self.sparse:
-            self.rows_sent += n_out
-            recv = torch.empty(n_in * W, dtype=torch.int64, device=send.device)
-            return self._a2a(recv, send[:n_out * W], [int(c) * W for c in recv_counts],
-                             [int(c) * W for c in send_counts])
-        mask, rows, live = live_rows(send, send_counts, W)
-        self.rows_sent += int(live.sum())
-        dev = send.device
-        cnt = torch.as_tensor(live, dtype=torch.int64, device=dev)
-        got = self._a2a(torch.empty(len(recv_counts), dtype=torch.int64, device=dev), cnt,
-                        [1] * len(recv_counts), [1] * len(send_counts)).cpu().numpy()
-        rmask = self._a2a(torch.empty(n_in, dtype=torch.uint8, device=dev), mask,
-                          [int(c) for c in recv_counts], [int(c) for c in send_counts])
-        rrows = self._a2a(torch.empty(int(got.sum()) * W, dtype=torch.int64, device=dev), rows,
-                          [int(c) * W for c in got], [int(c) * W for c in live])
-        return expand_rows(rmask, rrows, W)
-
-    def allreduce_sum(self, values):
+    def exchange_counts(self, vec):
         torch, dist = self.torch, self.dist
         dev = self.device if self.backend == "nccl" else "cpu"
-        t = torch.tensor(np.asarray(values, dtype=np.int64), device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
-        return t.cpu().numpy()
+        t = torch.as_tensor(np.asarray(vec, dtype=np.int64), device=dev)
+        out = torch.empty(self.world * t.numel(), dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(out, t, group=self.group)
+        return out.cpu().numpy().reshape(self.world, -1)
+
+    def exchange_records(self, send_buf, send_off, send_cnt, recv_buf, recv_cnt, R):
+        """send_buf: records to rank q at record send_off[q], send_cnt[q] of them; recv_buf:
+        the records from every source rank, packed in source order (R int64 per record)."""
+        torch, dist = self.torch, self.dist
+        recv_off = np.concatenate([[0], np.cumsum(recv_cnt)]).astype(np.int64)
+        stage = self.backend != "nccl" and send_buf.is_cuda  # gloo moves host tensors only
+        ops, landing = [], []
+        for q in range(self.world):
+            if q == self.rank:
+                continue
+            if send_cnt[q]:
+                x = send_buf[int(send_off[q]) * R:(int(send_off[q]) + int(send_cnt[q])) * R]
+                ops.append(dist.P2POp(dist.isend, x.cpu() if stage else x, q, group=self.group))
+            if recv_cnt[q]:
+                y = recv_buf[int(recv_off[q]) * R:int(recv_off[q + 1]) * R]
+                buf = torch.empty(y.shape, dtype=y.dtype) if stage else y
+                ops.append(dist.P2POp(dist.irecv, buf, q, group=self.group))
+                if stage:
+                    landing.append((y, buf))
+        if ops:
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
+        for y, buf in landing:
+            y.copy_(buf)
 
 
 class PartitionedNetwork:
-    """The relay of ``GraphNetwork`` on one rank of a vertex-partitioned multi-GPU job."""
+    """The relay of ``GraphNetwork`` on one rank of a vertex-partitioned multi-GPU job.
+
+    Per round r (``step``): finish round r on this rank (``p2pg_step_end``), pack its live
+    boundary rows on the device (``p2pg_exchange_pack_live``: one record per row that carries
+    something, counted per destination), one all-gather of (record counts, round counters),
+    then -- while the grouped sends / receives of the records are in flight -- the interior
+    peers of round r+1 (no ghost neighbour) already run (``p2pg_step_begin``); the records are
+    unpacked (``p2pg_exchange_unpack_live``) before the border peers of round r+1 run."""
 
     def __init__(self, graph, world, rank, transport, mode="flood", fanout=3, gossip_seed=0x5EED,
                  churn_threshold_value=0, churn_seed=0xC0FFEE, record=False, timing=False,
-                 device=0, engine_factory=None):
+                 device=0, engine_factory=None, overlap=True):
         if record and mode == "gossip" and world > 1:
             # a gossip parent check needs the REMOTE sender's degree and adjacency order
             raise NotImplementedError("record=True for partitioned gossip: record on one GPU")
-        self.graph, self.world, self.rank, self.transport = graph, world, rank, transport
+        self.world, self.rank, self.transport = world, rank, transport
+        self.deg = graph.degree().astype(np.int32)  # global degrees (round-0 counters); the
+        # global graph itself is not kept: the engine holds only the rank-local CSR
         self.mode, self.fanout = mode, fanout
+        self.overlap = overlap
         self.part = VertexPartition(graph, world, rank)
         make = engine_factory or GraphNetwork
         self.net = make(self.part.local_graph(), mode=mode, fanout=fanout, gossip_seed=gossip_seed,
@@ -193,10 +178,13 @@ class PartitionedNetwork:
                         local_graph=True)
         self.net.set_global_ids(self.part.gid)
         self.net.set_exchange(self.part.send_local, self.part.recv_local)
+        self.net.set_exchange_segments(self.part.send_counts, self.part.recv_counts)
         self.rounds = []        # global counters (summed over ranks)
         self.local_rounds = []  # this rank's engine counters (its owned peers' work)
         self.exchange_s = 0.0   # host wall time spent in the row exchange since reset
         self.sources = None
+        self._begun = False
+        self._bufs = None
 
     @property
     def M(self):
@@ -206,14 +194,19 @@ class PartitionedNetwork:
         self.sources = np.asarray(sources, dtype=np.int64)
         self.net.broadcast(self.part.local_sources(self.sources))
         self.rounds, self.local_rounds, self.exchange_s = [], [], 0.0
+        self._begun = False
+        W = (self.M + 63) // 64
+        rows = max(len(self.part.send_local), len(self.part.recv_local), 1)
+        self._bufs = (self.net.alloc_exchange(rows * (1 + W)), self.net.alloc_exchange(rows * (1 + W)))
 
     def reset(self):
         self.net.reset()
         self.rounds, self.local_rounds, self.exchange_s = [], [], 0.0
+        self._begun = False
 
     def _round0_stats(self):
         """Origination counted once, globally (every rank seeds origins it holds as ghosts)."""
-        deg = self.graph.degree()
+        deg = self.deg.astype(np.int64)
         src = self.sources
         W = (self.M + 63) // 64
         per = np.minimum(deg[src], self.fanout) if self.mode == "gossip" else deg[src]
@@ -226,43 +219,48 @@ class PartitionedNetwork:
 
     @staticmethod
     def _ready(t):
-        """The transport builds the received rows with torch ops on torch's current stream; the
+        """Records received with torch ops / RCCL are ordered on torch's current stream; the
         engine unpacks on its own stream, so wait for them first (nothing else orders them)."""
         if getattr(t, "is_cuda", False):
             import torch
             torch.cuda.current_stream(t.device).synchronize()
         return t
 
-    def _exchange(self):
-        if self.world == 1:
-            return
-        W = (self.M + 63) // 64
-        p = self.part
-        if self.mode == "flood":   # frontier rows: owner -> ghost holders
-            send = self.net.alloc_exchange(int(p.send_counts.sum()) * W)
-            self.net.exchange_pack(0, send)
-            recv = self.transport.alltoall_rows(send, p.send_counts, p.recv_counts, W)
-            self.net.exchange_unpack(0, self._ready(recv))
-        else:                      # gossip pushes: ghost holder -> owner
-            send = self.net.alloc_exchange(int(p.recv_counts.sum()) * W)
-            self.net.exchange_pack(1, send)
-            recv = self.transport.alltoall_rows(send, p.recv_counts, p.send_counts, W)
-            self.net.exchange_unpack(1, self._ready(recv))
-
     def step(self):
-        st = self.net.step()
+        if not self._begun:
+            self.net.step_begin()
+        st = self.net.step_end()
+        self._begun = False
         self.local_rounds.append(st)
-        t0 = time.perf_counter()
-        self._exchange()
-        self.exchange_s += time.perf_counter() - t0
+        vals = np.asarray([getattr(st, f) for f in STAT_FIELDS[2:]], dtype=np.int64)
+        if self.world == 1:
+            tot = vals
+        else:
+            t0 = time.perf_counter()
+            W = (self.M + 63) // 64
+            R = 1 + W
+            p = self.part
+            plane = 0 if self.mode == "flood" else 1
+            # plane 0: frontier rows owner -> ghost holders; plane 1: pushes ghost -> owner
+            send_rows, recv_rows = (p.send_counts, p.recv_counts) if plane == 0 else (p.recv_counts, p.send_counts)
+            send_off = np.concatenate([[0], np.cumsum(send_rows)]).astype(np.int64)
+            sbuf, rbuf = self._bufs
+            counts = np.asarray(self.net.exchange_pack_live(plane, sbuf), dtype=np.int64)
+            allv = self.transport.exchange_counts(np.concatenate([counts, vals]))
+            recv_cnt = allv[:, self.rank].copy()
+            tot = allv[:, self.world:].sum(axis=0)
+            self.transport.rows_total += int(send_rows.sum())
+            self.transport.rows_sent += int(counts.sum())
+            if self.overlap and tot[0] > 0:
+                self.net.step_begin()  # round r+1's interior peers, while the records travel
+                self._begun = True
+            self.transport.exchange_records(sbuf, send_off, counts, rbuf, recv_cnt, R)
+            self.net.exchange_unpack_live(plane, self._ready(rbuf), recv_cnt)
+            self.exchange_s += time.perf_counter() - t0
         if st.round == 0:
             g = self._round0_stats()
-            # scatter words of round 0 are real local work (gossip): sum them
-            sw = int(self.transport.allreduce_sum([st.scatter_words])[0]) if self.world > 1 else st.scatter_words
-            g.scatter_words = sw
+            g.scatter_words = int(tot[STAT_FIELDS[2:].index("scatter_words")])
         else:
-            vals = [getattr(st, f) for f in STAT_FIELDS[2:]]
-            tot = self.transport.allreduce_sum(vals) if self.world > 1 else np.asarray(vals)
             g = RoundStats(st.round, int(tot[0] > 0), *[int(x) for x in tot])
         self.rounds.append(g)
         return g

@@ -41,6 +41,16 @@ class MockEngine:
     def set_exchange(self, send_local, recv_local):
         self.send, self.recv = np.asarray(send_local), np.asarray(recv_local)
 
+    def set_exchange_segments(self, send_counts, recv_counts):
+        self.send_off = np.concatenate([[0], np.cumsum(send_counts)]).astype(np.int64)
+        self.recv_off = np.concatenate([[0], np.cumsum(recv_counts)]).astype(np.int64)
+
+    def step_begin(self):
+        pass
+
+    def step_end(self):
+        return self.step()
+
     def alloc_exchange(self, n_words):
         import torch
         return torch.zeros(max(int(n_words), 1), dtype=torch.int64)
@@ -150,6 +160,49 @@ class MockEngine:
             # a boundary peer appears once per neighbouring rank: OR, never overwrite
             # (the device unpack uses atomicOr); gossip parents are not checked when partitioned
             np.logical_or.at(self.next, self.send, b)
+
+    def exchange_pack_live(self, plane, buf):
+        """The compacted records of include/p2pgpu.h p2pg_exchange_pack_live."""
+        import torch
+        W = (self.M + 63) // 64
+        R = 1 + W
+        if plane == 0:
+            ids, off, rows = self.send, self.send_off, self.F[self.send]
+        else:
+            ids, off, rows = self.recv, self.recv_off, self.next[self.recv].copy()
+            self.next[self.recv] = False
+        words = _words(rows).astype(np.int64) if len(ids) else np.zeros((0, W), np.int64)
+        counts = np.zeros(len(off) - 1, dtype=np.int64)
+        out = buf.numpy() if not buf.is_cuda else None
+        recs = np.zeros_like(out) if out is None else out
+        for q in range(len(off) - 1):
+            for i in range(off[q], off[q + 1]):
+                if not rows[i].any():
+                    continue
+                r = (off[q] + counts[q]) * R
+                recs[r] = i - off[q]
+                recs[r + 1:r + R] = words[i]
+                counts[q] += 1
+        if out is None:
+            buf.copy_(torch.from_numpy(recs))
+        return counts
+
+    def exchange_unpack_live(self, plane, buf, counts):
+        arr = buf.cpu().numpy().astype(np.int64)
+        W = (self.M + 63) // 64
+        R = 1 + W
+        ids, off = (self.recv, self.recv_off) if plane == 0 else (self.send, self.send_off)
+        i = 0
+        for p, n in enumerate(counts):
+            for _ in range(int(n)):
+                rec = arr[i * R:(i + 1) * R]
+                v = ids[off[p] + rec[0]]
+                b = _bits(rec[1:].view(np.uint64).reshape(1, W), self.M)[0]
+                if plane == 0:
+                    self.F[v] = b
+                else:  # a boundary peer can be pushed to from several ranks: OR
+                    self.next[v] |= b
+                i += 1
 
     def deliveries(self, cap=None):
         """this round's first receipts (unordered contract: callers sort)"""

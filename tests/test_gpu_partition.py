@@ -14,10 +14,12 @@ pytestmark = pytest.mark.gpu
 
 
 class ThreadTransport:
-    """all-to-all / sum-reduce among `world` threads of one process (device tensors)."""
+    """The transport contract of PartitionedNetwork among `world` threads of one process
+    (device tensors): an all-gather of count vectors and the record sends / receives."""
 
-    def __init__(self, shared, rank, sparse=True):
-        self.s, self.rank, self.sparse = shared, rank, sparse
+    def __init__(self, shared, rank):
+        self.s, self.rank = shared, rank
+        self.rows_total = self.rows_sent = 0
 
     def _gather(self, item):
         s = self.s
@@ -27,44 +29,30 @@ class ThreadTransport:
         s["barrier"].wait()
         return items
 
-    def alltoall_rows(self, send, send_counts, recv_counts, W):
-        import torch
-        from p2pnetwork.gpu.partition import expand_rows, live_rows
+    def exchange_counts(self, vec):
+        return np.stack(self._gather(np.asarray(vec, dtype=np.int64)))
+
+    def exchange_records(self, send_buf, send_off, send_cnt, recv_buf, recv_cnt, R):
         # no extra synchronisation: the production ordering (PartitionedNetwork._ready) is tested
-        if self.sparse:  # the TorchTransport protocol: row flags + live rows only
-            mask, rows, live = live_rows(send, send_counts, W)
-            items = self._gather((mask, rows, np.asarray(send_counts), live))
-            mp, rp = [], []
-            for m, r, counts, lv in items:
-                off = int(counts[:self.rank].sum())
-                mp.append(m[off:off + int(counts[self.rank])])
-                loff = int(lv[:self.rank].sum()) * W
-                rp.append(r[loff:loff + int(lv[self.rank]) * W])
-            out = expand_rows(torch.cat(mp), torch.cat(rp), W)
-            assert out.numel() == int(np.sum(recv_counts)) * W
-            return out
-        items = self._gather((send, np.asarray(send_counts)))
-        pieces = []
-        for buf, counts in items:
-            off = int(counts[:self.rank].sum()) * W
-            pieces.append(buf[off:off + int(counts[self.rank]) * W])
-        out = torch.cat(pieces) if pieces else send[:0]
-        assert out.numel() == int(np.sum(recv_counts)) * W
-        return out
-
-    def allreduce_sum(self, values):
-        items = self._gather(np.asarray(values, dtype=np.int64))
-        return np.sum(items, axis=0)
+        items = self._gather((send_buf, np.asarray(send_off), np.asarray(send_cnt)))
+        off = 0
+        for p, (buf, so, sc) in enumerate(items):
+            n = int(sc[self.rank]) if p != self.rank else 0
+            assert n == int(recv_cnt[p]) or p == self.rank
+            if n:
+                recv_buf[off * R:(off + n) * R].copy_(buf[int(so[self.rank]) * R:(int(so[self.rank]) + n) * R])
+                off += n
+        self.s["barrier"].wait()  # every rank has copied out of the send buffers
 
 
-def run_partitioned(g, world, src, sparse=True, **kw):
+def run_partitioned(g, world, src, overlap=True, **kw):
     from p2pnetwork.gpu import PartitionedNetwork
     shared = {"slots": [None] * world, "barrier": threading.Barrier(world)}
     results, errors = [None] * world, []
 
     def rank_main(rank):
         try:
-            net = PartitionedNetwork(g, world, rank, ThreadTransport(shared, rank, sparse), **kw)
+            net = PartitionedNetwork(g, world, rank, ThreadTransport(shared, rank), overlap=overlap, **kw)
             with net.net:
                 net.broadcast(src)
                 rounds = net.run()
@@ -101,7 +89,7 @@ def graph(kind):
     return PeerGraph.gnp(5_000, 1.5, seed=2)                   # many small components
 
 
-@pytest.mark.parametrize("kind,mode,M,thr,world,sparse", [
+@pytest.mark.parametrize("kind,mode,M,thr,world,overlap", [
     ("ws", "flood", 64, 0, 2, True),
     ("ws", "flood", 64, 0, 2, False),
     ("ws", "flood", 130, 400_000_000, 3, True),
@@ -112,14 +100,15 @@ def graph(kind):
     ("ba", "gossip", 96, 300_000_000, 3, True),
     ("sparse", "gossip", 40, 0, 4, True),
 ])
-def test_partitioned_engines_match_single_gpu(kind, mode, M, thr, world, sparse):
-    """Real engines as threads == one engine == the C oracle; compacted row exchange (only
-    boundary rows with a non-zero word travel) and whole rows."""
+def test_partitioned_engines_match_single_gpu(kind, mode, M, thr, world, overlap):
+    """Real engines as threads == one engine == the C oracle; compacted record exchange (only
+    boundary rows with a non-zero word travel), with the next round's interior peers running
+    while the records are exchanged (overlap) and without."""
     from p2pnetwork.gpu import GraphNetwork, make_sources
     g = graph(kind)
     src = make_sources(g.V, M, seed=21)
     kw = dict(mode=mode, fanout=3, gossip_seed=99, churn_threshold_value=thr, churn_seed=17)
-    res = run_partitioned(g, world, src, sparse=sparse, record=(mode == "flood"), **kw)
+    res = run_partitioned(g, world, src, overlap=overlap, record=(mode == "flood"), **kw)
     with GraphNetwork(g, record=True, **kw) as one:
         one.broadcast(src)
         rounds1 = one.run()
