@@ -107,3 +107,43 @@ def test_gossip_full_width_1m_matches_c_oracle(push, monkeypatch):
     ora = coracle.run(g.rowptr, g.colidx, src, "gossip", 3, GSEED, record=False, want_seen=True)
     np.testing.assert_array_equal(seen, ora.seen)
     assert_rounds_equal(rounds, ora.rounds)
+
+
+def _hub_graph(V, m, seed):
+    """Power-law graph plus two stars wider than the pull hub threshold (deg > 512): hub
+    senders push through chunk items, hub receivers pull through k_pull_hub_*, and rows of
+    64 < deg <= 512 walk their slot words 64 at a time."""
+    from p2pnetwork.gpu import PeerGraph
+    g = PeerGraph.barabasi_albert(V, m, seed)
+    rows = np.repeat(np.arange(g.V), g.degree())
+    keep = rows < g.colidx
+    e = list(zip(rows[keep].tolist(), g.colidx[keep].tolist()))
+    e += [(7, j) for j in range(100, 2100)]
+    e += [(V - 1, j) for j in range(0, V - 1, 97)]
+    return PeerGraph.from_edges(g.V, e)
+
+
+@pytest.mark.parametrize("push", ["auto", "store_unfused"])
+@pytest.mark.parametrize("V,M,fanout,churn", [(200_000, 1500, 3, 0.1), (120_000, 2048, 4, 0.0)])
+def test_gossip_wide_rows_hubs_churn_match_c_oracle(V, M, fanout, churn, push, monkeypatch):
+    """Rows of 24 and 32 words (W > 16: one peer per wave, packed E rows and slot words) with
+    a ragged last word, churn (lost sends leave their slot word empty) and hubs: the whole
+    seen plane and every per-round counter == the C oracle, fused and unfused."""
+    from p2pnetwork.gpu import GraphNetwork, make_sources
+    from p2pnetwork.gpu.network import churn_threshold
+    monkeypatch.setenv("P2PG_GOSSIP_PUSH", "auto")
+    monkeypatch.setenv("P2PG_FUSED", "0" if push == "store_unfused" else "1")
+    g = _hub_graph(V, 4, seed=V + M)
+    src = make_sources(g.V, M, seed=7)
+    thr = churn_threshold(churn) if churn else 0
+    with GraphNetwork(g, mode="gossip", fanout=fanout, gossip_seed=GSEED,
+                      churn_threshold_value=thr, churn_seed=CSEED) as net:
+        net.broadcast(src)
+        rounds = net.run()
+        seen = net.seen_plane()
+    forms = {r.push_form for r in rounds if r.new_deliveries}
+    assert (3 if push == "auto" else 2) in forms, forms  # dense rounds ran
+    ora = coracle.run(g.rowptr, g.colidx, src, "gossip", fanout, GSEED, churn_threshold=thr,
+                      churn_seed=CSEED, record=False, want_seen=True)
+    np.testing.assert_array_equal(seen, ora.seen)
+    assert_rounds_equal(rounds, ora.rounds)
