@@ -73,6 +73,9 @@ struct p2pg_engine {
                                // rows: word density alone is high whenever anything is active)
   int push_mode = 0;           // 0 auto, 1 always row atomics, 2 always edge stores
   bool fused = true;           // dense rounds after dense rounds: one pull+scatter pass
+  bool skip_frontier = false;  // p2pg_run, not its last two allowed rounds: fused rounds may skip F
+  bool frontier_kept = true;   // F[(round-1)&1] holds the last round's first receipts
+  bool frontier_kept_prev = true;  // ... and F[round&1] the round before (delivery parents)
   uint64_t prev_aw = 0, prev_av = 0;  // active words / rows of the previous round
   int32_t* d_src = nullptr;
   DevState st{};
@@ -219,6 +222,7 @@ RoundParams params(const p2pg_engine* e) {
   p.cseed_hi = (uint32_t)(e->cfg.churn_seed >> 32);
   p.border = nullptr;
   p.phase = -1;
+  p.store_f = 1;
   return p;
 }
 
@@ -555,6 +559,8 @@ int p2pg_reset(p2pg_engine* e) {
   e->round = 0;
   e->done = false;
   e->begun = false;
+  e->frontier_kept = true;
+  e->frontier_kept_prev = true;
   e->last_push_e = false;
   e->consume_next = false;
   e->total_relays = 0;
@@ -668,6 +674,9 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
          (double)e->prev_av >= e->v_thresh * (double)e->V);
     fused_round = !e->d_gid && dense_pred && gossip_fused_supported(s);
     if (fused_round) {
+      // a frontier nobody observes is not stored: inside p2pg_run (not its last allowed
+      // round), without hop/parent records
+      p.store_f = (e->skip_frontier && !s.hop) ? 0 : 1;
       if ((rc = timed(e, 7, [&] {
              return launch_gossip_fused(g, s, p, e->hp, e->d_hub_big, e->n_hub_big, e->stream);
            })))
@@ -738,6 +747,8 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
   }
 #endif
   const bool active = tot[ST_NEW] != 0;
+  e->frontier_kept_prev = e->frontier_kept;
+  e->frontier_kept = !(fused_round && !p.store_f && active);
   if (out) {
     out->round = e->round;
     out->active = active ? 1 : 0;
@@ -770,7 +781,12 @@ int p2pg_run(p2pg_engine* e, int32_t max_rounds, p2pg_round_stats* per_round,
   int rc = 1;
   while (n < max_rounds) {
     p2pg_round_stats tmp;
+    // only the last two rounds a call may run can leave frontiers behind for the caller (the
+    // deliveries of the last round and their parents in the round before; snapshots); a
+    // quiescent round has none
+    e->skip_frontier = n + 2 < max_rounds;
     rc = p2pg_step(e, per_round ? &per_round[n] : &tmp);
+    e->skip_frontier = false;
     if (rc < 0) return rc;
     ++n;
     if (rc == 0) break;
@@ -785,6 +801,8 @@ int p2pg_get_new_deliveries(p2pg_engine* e, int64_t cap, int32_t* peer, int32_t*
     return fail(e, P2PG_ERR_ARG, "get_new_deliveries: bad arguments");
   if (!e->have_state || e->round == 0)
     return fail(e, P2PG_ERR_STATE, "get_new_deliveries: no round has run");
+  if (!e->frontier_kept || !e->frontier_kept_prev)
+    return fail(e, P2PG_ERR_STATE, "get_new_deliveries: the last rounds' frontiers were not kept");
   HIPCHK(e, hipSetDevice(e->cfg.device));
   // the most recent round is e->round - 1; its frontier is F[(round-1)&1]
   RoundParams p = params(e);
@@ -1227,6 +1245,8 @@ int p2pg_snapshot(p2pg_engine* e, void* buf, int64_t cap) {
   if (!e->have_state) return fail(e, P2PG_ERR_STATE, "snapshot: no sources set");
   if (e->arr_round >= 0 && e->arr_round == e->round)
     return fail(e, P2PG_ERR_STATE, "snapshot: take it before a topology update or after the next round");
+  if (!e->frontier_kept)
+    return fail(e, P2PG_ERR_STATE, "snapshot: the last round's frontier was not kept");
   HIPCHK(e, hipSetDevice(e->cfg.device));
   DevState& s = e->st;
   if (e->cfg.mode == P2PG_MODE_GOSSIP && e->last_push_e && e->round > 0 && !e->done) {

@@ -300,7 +300,7 @@ __global__ __launch_bounds__(256, P2PG_GROUPED_WAVES) void k_gossip_fused_groupe
       const uint64_t wm_all = __ballot(nw != 0ull);
       const uint32_t grp = (uint32_t)((wm_all >> (gl * WP)) & gmask);  // my peer's active words
       if (nw) st_frow(&st.seen[u * W + wl], a.s | nw);
-      if (mine && grp && wvalid) st_frow(&Fc[u * W + wl], nw);
+      if (mine && grp && wvalid && p.store_f) st_frow(&Fc[u * W + wl], nw);
       if (nw) {
         const uint32_t pc = (uint32_t)__popcll(nw);
         c[ST_NEW] += pc;

@@ -1292,7 +1292,7 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
         c[ST_WEDGES] += (uint32_t)deg;
       }
       if (wm) {
-        if (valid) st_frow(&Fc[u * W + lane], nw);
+        if (valid && p.store_f) st_frow(&Fc[u * W + lane], nw);
         aw |= 1u << a.b;
         if (lane == 0) {
           st.AW[cur][u] = wm;
