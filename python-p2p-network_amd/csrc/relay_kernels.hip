@@ -188,6 +188,22 @@ struct PullStage {
   uint32_t rv;      // fused gossip: receiver slot rev[j] of this lane's connection
 };
 
+// One target's prefetch stage for k_gossip_fused: as PullStage, with 32-bit peer and slot ids
+// (gossip slot ids are uint32: rev[]) -- the fused kernel's scalar registers are the scarce ones.
+struct FusedStage {
+  int b;            // 0 = a target, -1 = none
+  int32_t u;        // the target peer
+  uint32_t beg, end;
+  uint64_t s;
+  int32_t v;
+  uint32_t r;
+  bool act;
+  uint32_t aword;
+  uint64_t mr;
+  uint64_t am;
+  uint32_t rv;
+};
+
 // Word `lane` of a source row.  Packed E rows (gossip, st.AW) hold only the sender's active
 // words in order: word w sits at position popcount(am & ((1 << w) - 1)), absent if bit w of am
 // is clear (the sender had nothing in that word: the mask is zero).
@@ -1099,258 +1115,128 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
   uint64_t tot[STAT_N] = {0, 0, 0, 0, 0, 0, 0, 0};
   PROF_DECL
 
-  for (int64_t task = (int64_t)blockIdx.x * WPB + wib; task < ntasks;
-       task += (int64_t)gridDim.x * WPB) {
-    const int64_t u0 = task << 5;
-    const uint32_t sat0 = st.S[task];
-    uint32_t todo = ~sat0;
-    if (g.H) todo &= ~g.H[task];  // hubs: k_pull_hub_* items
-    if (V - u0 < 32) todo &= (1u << (V - u0)) - 1u;
-    if (!todo) {
-      if (lane == 0) st.A[cur][task] = 0u;
-      continue;
+  // Issuer (wave-uniform): this wave's tasks in grid-stride order and, in each, its
+  // unsaturated non-hub peers in ascending order.  The next task's saturated / hub words and
+  // row offsets are loaded while the current one is issued, so the software pipeline below runs
+  // straight across task boundaries (restarting it per 32-peer task cost 3-4 dependent memory
+  // trips: ~12 % of a light round).
+  const int64_t tstride = (int64_t)gridDim.x * WPB;
+  int64_t pf_task = (int64_t)blockIdx.x * WPB + wib;  // prefetched task (-1: none left)
+  uint32_t pf_s = 0, pf_h = 0;
+  uint32_t pf_rp = 0;  // slot offsets fit 32 bits (rev[] holds slot ids as uint32)
+  auto prefetch = [&](int64_t t) {
+    pf_task = t;
+    if (t < 0) return;
+    pf_s = st.S[t];
+    pf_h = g.H ? g.H[t] : 0u;
+    const int64_t u0 = t << 5;
+    pf_rp = (lane <= 32 && u0 + lane <= V) ? (uint32_t)g.rowptr[u0 + lane] : 0u;
+  };
+  if (pf_task >= ntasks) pf_task = -1;
+  prefetch(pf_task);
+  int32_t it_u0 = 0;     // first peer of the issuing task
+  uint32_t it_rest = 0;  // its peers not issued yet
+  uint32_t rp = 0;       // lane l <= 32: rowptr[it_u0 + l]
+  // next peer to issue (global id; -1 when this wave's tasks are done) and its slot range
+  auto next_peer = [&](uint32_t& beg, uint32_t& end) -> int32_t {
+    while (!it_rest) {
+      const int64_t t = pf_task;
+      if (t < 0) return -1;
+      const int64_t u0 = t << 5;
+      uint32_t todo = ~(uint32_t)__builtin_amdgcn_readfirstlane((int)pf_s) &
+                      ~(uint32_t)__builtin_amdgcn_readfirstlane((int)pf_h);
+      if (V - u0 < 32) todo &= (1u << (V - u0)) - 1u;
+      rp = pf_rp;
+      prefetch(t + tstride < ntasks ? t + tstride : -1);
+      if (!todo) {
+        if (lane == 0) st.A[cur][t] = 0u;
+        continue;
+      }
+      it_u0 = (int32_t)u0;
+      it_rest = todo;
     }
-    int64_t rp = 0;
-    if (lane <= 32 && u0 + lane <= V) rp = g.rowptr[u0 + lane];
+    const int b = __builtin_ctz(it_rest);
+    it_rest &= it_rest - 1u;
+    beg = (uint32_t)__builtin_amdgcn_readlane((int)rp, b);
+    end = (uint32_t)__builtin_amdgcn_readlane((int)rp, b + 1);
+    return it_u0 + b;
+  };
 
-    auto issue = [&](PullStage& q, int b) {
-      q.b = b;
-      q.act = false;
-      q.v = 0;
-      q.r = 0;
-      q.rv = 0;
-      q.s = 0;
-      if (b < 0) return;
-      q.beg = readlane64(rp, b);
-      q.end = readlane64(rp, b + 1);
-      if (valid) q.s = ld_once(&st.seen[(u0 + b) * W + lane]);
-      const int64_t j = q.beg + lane;
-      if (j < q.end) {
-        q.v = ld_once(&g.colidx[j]);
-        q.r = (uint32_t)j;
-        q.rv = ld_once(&g.rev[j]);
-      }
-    };
-    // loads only; gather() tests the bit (see k_pull1)
-    auto activity = [&](PullStage& q) {
-      if (q.b < 0) return;
-      const int64_t j = q.beg + lane;
-      q.am = 0;
-      q.aword = 0;
-      if (j < q.end) {
-        q.am = AWp[q.v];
-        q.aword = Ap[q.v >> 5];
-      }
-    };
-    auto next_bit = [](uint32_t& t) -> int {
-      if (!t) return -1;
-      const int b = __builtin_ctz(t);
-      t &= t - 1u;
-      return b;
-    };
-
-    // L4: the first FG active neighbours' words of q go out into X; mr = q's active slots
-    // (of its first 64) still to gather
-    uint64_t X[FG];
-    auto gather = [&](const PullStage& q, uint64_t& mr) {
-      const uint64_t needm = __ballot((fm & ~q.s) != 0ull);
-      const int64_t jq = q.beg + lane;
-      uint64_t m = __ballot(jq < q.end && ((q.aword >> (q.v & 31)) & 1u));
-      // all slot ids / word masks first, then all FG loads back to back: a readlane between
-      // two loads would make the wave wait for the first one (merged vmcnt state)
-      uint32_t sv[FG];
-      uint64_t am[FG];
-      bool ok[FG];
-#pragma unroll
-      for (int k = 0; k < FG; ++k) {
-        sv[k] = 0u;
-        am[k] = 0ull;
-        ok[k] = m != 0ull;
-        if (m) {
-          const int idx = __builtin_ctzll(m);
-          m &= m - 1ull;
-          sv[k] = (uint32_t)__builtin_amdgcn_readlane((int)q.r, idx);
-          am[k] = (uint64_t)readlane64((int64_t)q.am, idx);
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < FG; ++k) X[k] = src_word_m(Src, sv[k], W, am[k], ok[k] ? am[k] & needm : 0ull);
-      mr = m;
-    };
-
-    // Software pipeline, per target t: rows L2(t+2) -> activity L3(t+1) -> gathers(t) ->
-    // consume(t).  The first gathers of target t+1 are issued BEFORE target t's stores and
-    // picks, so their latency hides behind t's Philox / LDS work.  The four stages rotate by
-    // unrolling (step(A,B,C,D), step(B,C,D,A), ...), never by copying: a register copy of a
-    // load still in flight would make the wave wait for it (and, vmcnt being in order, for
-    // every younger load and store) at the end of each target.
-    uint32_t c[STAT_N] = {0, 0, 0, 0, 0, 0, 0, 0};
-    uint32_t aw = 0, sat = sat0;
-    uint32_t rest = todo;
-    // The flush (E stores) of a short row (deg <= GCHUNK) is deferred to the next target,
-    // after that target's gather wait: a wait issued right behind a row's stores would also
-    // wait for their completion (vmcnt counts loads and stores in order); one target later,
-    // the picks in between have covered it.
-    bool pend = false;
-    int64_t pu = 0, pbeg = 0, pdeg = 0;
-    uint64_t pnw = 0;
-    uint32_t prv = 0;
-    auto flush_pending = [&]() {
-      if (pend) {
-        scatter_row<CHURN, K, true, 2>(g, st, p, lds[wib], lane, pu, pbeg, pdeg, 0, 0, pnw, prv,
-                                       0, c PROF_PASS);
-        pend = false;
-      }
-    };
-    PullStage sA, sB, sC, sD;
-    issue(sA, next_bit(rest));
-    issue(sB, next_bit(rest));
-    activity(sA);
-    if (sA.b >= 0) gather(sA, sA.mr);
-    activity(sB);
-    issue(sC, next_bit(rest));
-    PROF_MARK(5);
-
-    // consume a (gathers in X), advance b (gathers), c (activity), d (rows), then a's picks
-    auto step = [&](PullStage& a, PullStage& b, PullStage& cc, PullStage& d) {
-      const int64_t u = u0 + a.b;
-      const uint64_t deg = (uint64_t)(a.end - a.beg);
-      const uint64_t need = fm & ~a.s;
-      const uint64_t needm = __ballot(need != 0ull);
-      uint64_t acc = 0;
-#pragma unroll
-      for (int k = 0; k < FG; ++k) acc |= X[k];
-      PROF_MARK(0);
-      {
-        uint64_t m = a.mr;  // the rest of the first 64 slots, then further 64-slot chunks
-        uint32_t srow = a.r;
-        uint64_t sam = a.am;
-        int64_t cb = a.beg;
-        for (;;) {
-          while (m) {
-            uint32_t sv[8];
-            uint64_t am[8];
-            bool ok[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-              ok[k] = m != 0ull;
-              am[k] = 0ull;
-              if (m) {
-                const int idx = __builtin_ctzll(m);
-                m &= m - 1ull;
-                sv[k] = (uint32_t)__builtin_amdgcn_readlane((int)srow, idx);
-                am[k] = (uint64_t)readlane64((int64_t)sam, idx);
-              } else {
-                sv[k] = 0u;
-              }
-            }
-            uint64_t x[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k)
-              x[k] = src_word_m(Src, sv[k], W, am[k], ok[k] ? am[k] & needm : 0ull);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) acc |= x[k];
-          }
-          cb += 64;
-          if (cb >= a.end) break;
-          const int64_t j = cb + lane;  // further chunks of a wide row: serial
-          bool act = false;
-          srow = 0;
-          sam = 0;
-          if (j < a.end) {
-            const int32_t v = g.colidx[j];
-            srow = (uint32_t)j;
-            act = bit_test(Ap, v);
-            if (act) sam = AWp[v];
-          }
-          m = __ballot(act);
-        }
-      }
-      // Everything loaded before this point (this target's rows, the next target's activity
-      // words) has landed or is about to: wait for it explicitly HERE, so that the compiler
-      // knows it has arrived and inserts no vmcnt wait behind the next target's gathers when
-      // this target's row words are used below (vmcnt is in order: such a wait would stall
-      // until those gathers return).
-      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-      PROF_MARK(1);
-      flush_pending();
-      // advance the pipeline before this target's stores and picks: gathers of t+1 (their
-      // activity words were loaded a target ago), activity words of t+2, rows of t+3
-      if (b.b >= 0) gather(b, b.mr);
-      activity(cc);
-      issue(d, next_bit(rest));
-      PROF_MARK(2);
-      const uint64_t nw = acc & need;
-      const uint64_t wm = __ballot(nw != 0ull);
-      if (nw) {
-        st_frow(&st.seen[u * W + lane], a.s | nw);
-        const uint32_t pc = (uint32_t)__popcll(nw);
-        const uint32_t per_bit = deg < (uint64_t)p.fanout ? (uint32_t)deg : (uint32_t)p.fanout;
-        c[ST_NEW] += pc;
-        c[ST_RELAYS] += pc * per_bit;
-        c[ST_ACTIVE_W] += 1;
-        c[ST_WEDGES] += (uint32_t)deg;
-      }
-      if (wm) {
-        if (valid && p.store_f) st_frow(&Fc[u * W + lane], nw);
-        aw |= 1u << a.b;
-        if (lane == 0) {
-          st.AW[cur][u] = wm;
-          c[ST_ACTIVE_W] += 1u << 16;  // ST_ACTIVE_V, packed (see the fold below)
-          c[ST_DEG_ACT] += (uint32_t)deg;
-        }
-        // this round's pushes, GCHUNK connections at a time.  a.rv holds the receiver slots of
-        // the first 64 (arrived: see the explicit wait above); wider rows load the next 64
-        // every 4 chunks and wait for them right there -- a load that MAY be in flight when
-        // the picks read the slots would make the compiler wait for everything, the next
-        // target's gathers included.
-        if (deg <= (uint64_t)GCHUNK) {
-          scatter_row<CHURN, K, true, 1>(g, st, p, lds[wib], lane, u, a.beg, (int64_t)deg, 0, 0,
-                                         nw, a.rv, 0, c PROF_PASS);
-          pend = true;
-          pu = u;
-          pbeg = a.beg;
-          pdeg = (int64_t)deg;
-          pnw = nw;
-          prv = a.rv;
-        } else if (deg <= 64) {
-          for (int ch = 0; (int64_t)ch * GCHUNK < (int64_t)deg; ++ch)
-            scatter_row<CHURN, K, true>(g, st, p, lds[wib], lane, u, a.beg, (int64_t)deg, ch, 0,
-                                        nw, a.rv, ch * GCHUNK, c PROF_PASS);
-        } else {
-          for (int ch = 0; (int64_t)ch * GCHUNK < (int64_t)deg; ++ch) {
-            const int off = (ch * GCHUNK) & 63;
-            const int64_t j = a.beg + (int64_t)(ch * GCHUNK - off) + lane;
-            const uint32_t rvb = j < a.end ? g.rev[j] : 0u;
-            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-            scatter_row<CHURN, K, true>(g, st, p, lds[wib], lane, u, a.beg, (int64_t)deg, ch, 0,
-                                        nw, rvb, off, c PROF_PASS);
-          }
-        }
-      }
-      PROF_MARK(3);
-      if (!__ballot(valid && (a.s | nw) != fm)) sat |= 1u << a.b;
-    };
-    for (;;) {
-      if (sA.b < 0) break;
-      step(sA, sB, sC, sD);
-      if (sB.b < 0) break;
-      step(sB, sC, sD, sA);
-      if (sC.b < 0) break;
-      step(sC, sD, sA, sB);
-      if (sD.b < 0) break;
-      step(sD, sA, sB, sC);
+  auto issue = [&](FusedStage& q) {
+    q.act = false;
+    q.v = 0;
+    q.r = 0;
+    q.rv = 0;
+    q.s = 0;
+    q.u = next_peer(q.beg, q.end);
+    q.b = q.u < 0 ? -1 : 0;
+    if (q.u < 0) return;
+    if (valid) q.s = ld_once(&st.seen[(int64_t)q.u * W + lane]);
+    const uint32_t j = q.beg + lane;
+    if (j < q.end) {
+      q.v = ld_once(&g.colidx[j]);
+      q.r = (uint32_t)j;
+      q.rv = ld_once(&g.rev[j]);
     }
-    flush_pending();
-    PROF_MARK(4);
+  };
+  // loads only; gather() tests the bit (see k_pull1)
+  auto activity = [&](FusedStage& q) {
+    if (q.b < 0) return;
+    const uint32_t j = q.beg + lane;
+    q.am = 0;
+    q.aword = 0;
+    if (j < q.end) {
+      q.am = AWp[q.v];
+      q.aword = Ap[q.v >> 5];
+    }
+  };
+
+  // the first FG active neighbours' words of q go out into X; mr = q's active slots (of its
+  // first 64) still to gather
+  uint64_t X[FG];
+  auto gather = [&](const FusedStage& q, uint64_t& mr) {
+    const uint64_t needm = __ballot((fm & ~q.s) != 0ull);
+    const uint32_t jq = q.beg + lane;
+    uint64_t m = __ballot(jq < q.end && ((q.aword >> (q.v & 31)) & 1u));
+    // all slot ids / word masks first, then all FG loads back to back: a readlane between
+    // two loads would make the wave wait for the first one (merged vmcnt state)
+    uint32_t sv[FG];
+    uint64_t am[FG];
+    bool ok[FG];
+#pragma unroll
+    for (int k = 0; k < FG; ++k) {
+      sv[k] = 0u;
+      am[k] = 0ull;
+      ok[k] = m != 0ull;
+      if (m) {
+        const int idx = __builtin_ctzll(m);
+        m &= m - 1ull;
+        sv[k] = (uint32_t)__builtin_amdgcn_readlane((int)q.r, idx);
+        am[k] = (uint64_t)readlane64((int64_t)q.am, idx);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < FG; ++k) X[k] = src_word_m(Src, sv[k], W, am[k], ok[k] ? am[k] & needm : 0ull);
+    mr = m;
+  };
+
+  // Per consumed task: activity word, newly saturated peers and the per-lane counters (32-bit,
+  // <= 32 peers per fold, none a hub: no overflow), folded into wave-uniform 64-bit totals when
+  // the consumer moves on to the next task.
+  uint32_t c[STAT_N] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int64_t ct = -1;
+  uint32_t aw = 0, nsat = 0;
+  auto finish_task = [&]() {
+    if (ct < 0) return;
     if (lane == 0) {
-      st.A[cur][task] = aw;
-      if (sat != sat0) st.S[task] = sat;
+      st.A[cur][ct] = aw;
+      if (nsat) atomicOr(&st.S[ct], nsat);  // this wave owns the task: no other writer
     }
 #pragma unroll
     for (int q = 0; q < STAT_N; ++q) {
       if (q == ST_ACTIVE_V) continue;
       const uint32_t r = wave_reduce_u32<false>(c[q]);
+      c[q] = 0;
       if (q == ST_ACTIVE_W) {
         // one register for two per-task counts (each <= 64 lanes x 32 peers < 2^16): active
         // words in the low half, active peers (lane 0) in the high half
@@ -1360,7 +1246,177 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
         tot[q] += r;
       }
     }
+    aw = 0;
+    nsat = 0;
+  };
+
+  // Software pipeline, per target t: rows L2(t+3) -> activity L3(t+2) -> gathers(t+1) ->
+  // consume(t).  The first gathers of target t+1 are issued BEFORE target t's stores and
+  // picks, so their latency hides behind t's Philox / LDS work.  The four stages rotate by
+  // unrolling (step(A,B,C,D), step(B,C,D,A), ...), never by copying: a register copy of a
+  // load still in flight would make the wave wait for it (and, vmcnt being in order, for
+  // every younger load and store) at the end of each target.
+  // The flush (E stores) of a short row (deg <= GCHUNK) is deferred to the next target,
+  // after that target's gather wait: a wait issued right behind a row's stores would also
+  // wait for their completion (vmcnt counts loads and stores in order); one target later,
+  // the picks in between have covered it.
+  bool pend = false;
+  int64_t pu = 0, pbeg = 0, pdeg = 0;
+  uint64_t pnw = 0;
+  uint32_t prcv = 0;  // its receiver slots
+  auto flush_pending = [&]() {
+    if (pend) {
+      scatter_row<CHURN, K, true, 2>(g, st, p, lds[wib], lane, pu, pbeg, pdeg, 0, 0, pnw, prcv,
+                                     0, c PROF_PASS);
+      pend = false;
+    }
+  };
+  FusedStage sA, sB, sC, sD;
+  issue(sA);
+  issue(sB);
+  activity(sA);
+  if (sA.b >= 0) gather(sA, sA.mr);
+  activity(sB);
+  issue(sC);
+  PROF_MARK(5);
+
+  // consume a (gathers in X), advance b (gathers), c (activity), d (rows), then a's picks
+  auto step = [&](FusedStage& a, FusedStage& b, FusedStage& cc, FusedStage& d) {
+    const int64_t u = a.u;
+    if ((u >> 5) != ct) {
+      finish_task();
+      ct = u >> 5;
+    }
+    const uint64_t deg = (uint64_t)(a.end - a.beg);
+    const uint64_t need = fm & ~a.s;
+    const uint64_t needm = __ballot(need != 0ull);
+    uint64_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < FG; ++k) acc |= X[k];
+    PROF_MARK(0);
+    {
+      uint64_t m = a.mr;  // the rest of the first 64 slots, then further 64-slot chunks
+      uint32_t srow = a.r;
+      uint64_t sam = a.am;
+      uint32_t cb = a.beg;
+      for (;;) {
+        while (m) {
+          uint32_t sv[8];
+          uint64_t am[8];
+          bool ok[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            ok[k] = m != 0ull;
+            am[k] = 0ull;
+            if (m) {
+              const int idx = __builtin_ctzll(m);
+              m &= m - 1ull;
+              sv[k] = (uint32_t)__builtin_amdgcn_readlane((int)srow, idx);
+              am[k] = (uint64_t)readlane64((int64_t)sam, idx);
+            } else {
+              sv[k] = 0u;
+            }
+          }
+          uint64_t x[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+            x[k] = src_word_m(Src, sv[k], W, am[k], ok[k] ? am[k] & needm : 0ull);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) acc |= x[k];
+        }
+        cb += 64;
+        if (cb >= a.end) break;
+        const uint32_t j = cb + lane;  // further chunks of a wide row: serial
+        bool act = false;
+        srow = 0;
+        sam = 0;
+        if (j < a.end) {
+          const int32_t v = g.colidx[j];
+          srow = (uint32_t)j;
+          act = bit_test(Ap, v);
+          if (act) sam = AWp[v];
+        }
+        m = __ballot(act);
+      }
+    }
+    // Everything loaded before this point (this target's rows, the next target's activity
+    // words, the prefetched task words) has landed or is about to: wait for it explicitly
+    // HERE, so that the compiler knows it has arrived and inserts no vmcnt wait behind the next
+    // target's gathers when this target's row words are used below (vmcnt is in order: such a
+    // wait would stall until those gathers return).
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    PROF_MARK(1);
+    flush_pending();
+    // advance the pipeline before this target's stores and picks: gathers of t+1 (their
+    // activity words were loaded a target ago), activity words of t+2, rows of t+3
+    if (b.b >= 0) gather(b, b.mr);
+    activity(cc);
+    issue(d);
+    PROF_MARK(2);
+    const uint64_t nw = acc & need;
+    const uint64_t wm = __ballot(nw != 0ull);
+    if (nw) {
+      st_frow(&st.seen[u * W + lane], a.s | nw);
+      const uint32_t pc = (uint32_t)__popcll(nw);
+      const uint32_t per_bit = deg < (uint64_t)p.fanout ? (uint32_t)deg : (uint32_t)p.fanout;
+      c[ST_NEW] += pc;
+      c[ST_RELAYS] += pc * per_bit;
+      c[ST_ACTIVE_W] += 1;
+      c[ST_WEDGES] += (uint32_t)deg;
+    }
+    if (wm) {
+      if (valid && p.store_f) st_frow(&Fc[u * W + lane], nw);
+      aw |= 1u << (u & 31);
+      if (lane == 0) {
+        st.AW[cur][u] = wm;
+        c[ST_ACTIVE_W] += 1u << 16;  // ST_ACTIVE_V, packed (see finish_task)
+        c[ST_DEG_ACT] += (uint32_t)deg;
+      }
+      // this round's pushes, GCHUNK connections at a time.  a.rv holds the receiver slots of
+      // the first 64 (arrived: see the explicit wait above); wider rows load the next 64
+      // every 4 chunks and wait for them right there -- a load that MAY be in flight when
+      // the picks read the slots would make the compiler wait for everything, the next
+      // target's gathers included.
+      if (deg <= (uint64_t)GCHUNK) {
+        scatter_row<CHURN, K, true, 1>(g, st, p, lds[wib], lane, u, a.beg, (int64_t)deg, 0, 0,
+                                       nw, a.rv, 0, c PROF_PASS);
+        pend = true;
+        pu = u;
+        pbeg = a.beg;
+        pdeg = (int64_t)deg;
+        pnw = nw;
+        prcv = a.rv;
+      } else if (deg <= 64) {
+        for (int ch = 0; (int64_t)ch * GCHUNK < (int64_t)deg; ++ch)
+          scatter_row<CHURN, K, true>(g, st, p, lds[wib], lane, u, a.beg, (int64_t)deg, ch, 0,
+                                      nw, a.rv, ch * GCHUNK, c PROF_PASS);
+      } else {
+        for (int ch = 0; (int64_t)ch * GCHUNK < (int64_t)deg; ++ch) {
+          const int off = (ch * GCHUNK) & 63;
+          const uint32_t j = a.beg + (uint32_t)(ch * GCHUNK - off) + lane;
+          const uint32_t rvb = j < a.end ? g.rev[j] : 0u;
+          __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+          scatter_row<CHURN, K, true>(g, st, p, lds[wib], lane, u, a.beg, (int64_t)deg, ch, 0,
+                                      nw, rvb, off, c PROF_PASS);
+        }
+      }
+    }
+    PROF_MARK(3);
+    if (!__ballot(valid && (a.s | nw) != fm)) nsat |= 1u << (u & 31);
+  };
+  for (;;) {
+    if (sA.b < 0) break;
+    step(sA, sB, sC, sD);
+    if (sB.b < 0) break;
+    step(sB, sC, sD, sA);
+    if (sC.b < 0) break;
+    step(sC, sD, sA, sB);
+    if (sD.b < 0) break;
+    step(sD, sA, sB, sC);
   }
+  flush_pending();
+  finish_task();
+  PROF_MARK(4);
   PROF_FLUSH
   if (lane == 0) {
     unsigned long long* shard = st.stats + (blockIdx.x & (STAT_SHARDS - 1)) * STAT_N;
