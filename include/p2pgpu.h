@@ -124,11 +124,16 @@ int p2pg_set_sources(p2pg_engine* e, int32_t M, const int32_t* src);
 int p2pg_reset(p2pg_engine* e);
 /* One round. Returns 1 while messages are in flight, 0 when quiescent, < 0 on error. */
 int p2pg_step(p2pg_engine* e, p2pg_round_stats* out);
-/* Rounds until quiescence or max_rounds; per_round may be NULL (else >= max_rounds slots). */
+/* Rounds until quiescence or max_rounds; per_round may be NULL (else >= max_rounds slots).
+ * Inside a call, fused dense gossip rounds other than the last two it may run do not store
+ * their frontier rows (no later round reads them), so the delivery stream is available for
+ * the last round a call ran, as after p2pg_step.                                          */
 int p2pg_run(p2pg_engine* e, int32_t max_rounds, p2pg_round_stats* per_round,
              int32_t* n_rounds);
 /* The first receipts of the most recent round, sorted by (peer, msg); parent = -1 at the
- * source.  Writes min(cap, count) records; *n_out = count (may exceed cap).             */
+ * source.  Writes min(cap, count) records; *n_out = count (may exceed cap).
+ * P2PG_ERR_STATE if that round's (or, for the parents, the previous round's) frontier was
+ * not kept -- not reachable through p2pg_step / p2pg_run as specified above.               */
 int p2pg_get_new_deliveries(p2pg_engine* e, int64_t cap, int32_t* peer, int32_t* msg,
                             int32_t* hop, int32_t* parent, int64_t* n_out);
 /* Validation copies: seen [V][W] uint64 (W = ceil(M/64)); hop/parent [V][M] int32 need
