@@ -15,6 +15,11 @@ namespace p2pg {
 namespace {
 
 constexpr int WPB = 4;  // waves per block (256 threads)
+// Sparse-round kernels scan this many task words per wave pass, one per lane
+#ifndef P2PG_SCAN_W
+#define P2PG_SCAN_W 4
+#endif
+constexpr int SCAN_W = P2PG_SCAN_W;
 constexpr int GRID_MAX = 2048;
 
 __device__ __forceinline__ bool bit_test(const uint32_t* bm, int64_t v) {

@@ -606,6 +606,131 @@ __global__ __launch_bounds__(256) void k_gossip_update(DevGraph g, DevState st,
   flush_stats(st.stats, c, lane);
 }
 
+// The same update for single-slice rows (W <= 64), software-pipelined over the touched peers
+// of a wave's tasks: the push row of peer t+2 and the seen words of t+1 (where t+1's push row
+// is nonzero) are in flight while t is consumed, so a touched peer costs one memory round trip
+// instead of two in sequence; the next task's touched word is a scalar load issued one task
+// ahead (only this wave writes a task's T word, after reading it).  Same results as
+// k_gossip_update (every gossip test runs it).
+struct UpdStage {
+  int64_t u;   // touched peer (-1: none)
+  uint64_t x;  // this lane's push word
+  uint64_t s;  // this lane's seen word (where x != 0)
+};
+
+__global__ __launch_bounds__(256) void k_gossip_update1(DevGraph g, DevState st, RoundParams p) {
+  const int lane = threadIdx.x & 63;
+  const int wib = wave_in_block();
+  const int64_t V = g.V;
+  const int W = st.W;
+  const int cur = p.round & 1;
+  uint64_t* __restrict__ nx = st.next[cur];
+  uint64_t* __restrict__ Fc = st.F[cur];
+  uint32_t* __restrict__ Tc = st.T[cur];
+  const int64_t ntasks = (V + 31) >> 5;
+  const bool valid = lane < W;
+  uint64_t c[STAT_N] = {0, 0, 0, 0, 0, 0, 0, 0};
+
+  const int64_t tstride = (int64_t)gridDim.x * WPB;
+  int64_t pf_task = (int64_t)blockIdx.x * WPB + wib;
+  uint32_t pf_tw = pf_task < ntasks ? ldc(&Tc[pf_task]) : 0u;
+  int64_t it_task = 0;
+  uint32_t it_rest = 0;
+  auto next_peer = [&]() -> int64_t {
+    while (!it_rest) {
+      const int64_t t = pf_task;
+      if (t >= ntasks) return -1;
+      const uint32_t tw0 = pf_tw;
+      pf_task = t + tstride;
+      pf_tw = pf_task < ntasks ? ldc(&Tc[pf_task]) : 0u;
+      const uint32_t tw = tw0 & phase_mask(p, t);
+      if (!tw) {
+        if (lane == 0 && p.phase != 1) st.A[cur][t] = 0u;  // put_active(.., 0, ..)
+        continue;
+      }
+      if (lane == 0) Tc[t] = tw0 & ~tw;  // consumed (the other phase's bits stay)
+      it_task = t;
+      it_rest = tw;
+    }
+    const int b = __builtin_ctz(it_rest);
+    it_rest &= it_rest - 1u;
+    return (it_task << 5) + b;
+  };
+  auto issue_x = [&](UpdStage& q) {
+    q.u = next_peer();
+    q.x = 0;
+    q.s = 0;
+    if (q.u >= 0 && valid) q.x = nx[q.u * W + lane];
+  };
+  auto issue_s = [&](UpdStage& q) {
+    if (q.u >= 0 && q.x) q.s = st.seen[q.u * W + lane];
+  };
+
+  int64_t ct = -1;  // task of the consumed peers
+  uint32_t aw = 0;
+  auto finish_task = [&]() {
+    if (ct >= 0 && lane == 0) put_active(st.A[cur], ct, aw, p);
+    aw = 0;
+  };
+  auto consume = [&](const UpdStage& q) {
+    const int64_t u = q.u;
+    if ((u >> 5) != ct) {
+      finish_task();
+      ct = u >> 5;
+    }
+    const int64_t deg = ldc(g.rowptr + u + 1) - ldc(g.rowptr + u);
+    // relays per first receipt: gossip min(k, deg); flood (rows materialized by a topology
+    // update) deg - 1, the sender's connection being excluded (node.py:106-112)
+    const uint64_t fan = p.mode == 0 ? (uint64_t)(deg > 0 ? deg - 1 : 0)
+                                     : (uint64_t)(deg < p.fanout ? deg : p.fanout);
+    const uint64_t x = q.x, s = q.s;
+    if (x) {
+      st_prow(&nx[u * W + lane], 0ull);
+      c[ST_AUX] += 1;  // touched (pushed-to) words consumed
+    }
+    const uint64_t nw = x & ~s;
+    const uint64_t wm = __ballot(nw != 0ull);
+    if (wm && st.AW[cur] && lane == 0) st.AW[cur][u] = wm;
+    if (nw) st_prow(&st.seen[u * W + lane], s | nw);
+    if (valid && wm) st_prow(&Fc[u * W + lane], nw);
+    if (nw) {
+      const uint64_t pc = (uint64_t)__popcll(nw);
+      c[ST_NEW] += pc;
+      c[ST_RELAYS] += pc * fan;
+      c[ST_ACTIVE_W] += 1;
+      c[ST_WEDGES] += (uint64_t)deg;
+    }
+    if (wm) {
+      aw |= 1u << (u & 31);
+      if (lane == 0) {
+        c[ST_ACTIVE_V] += 1;
+        c[ST_DEG_ACT] += (uint64_t)deg;
+      }
+    }
+  };
+  // three stages rotate by unrolling (a register copy of a load in flight would wait for it)
+  auto step = [&](UpdStage& a, UpdStage& b, UpdStage& cc) {
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): a's seen words and b's push row landed
+    issue_s(b);
+    issue_x(cc);
+    consume(a);
+  };
+  UpdStage sA, sB, sC;
+  issue_x(sA);
+  issue_x(sB);
+  issue_s(sA);
+  for (;;) {
+    if (sA.u < 0) break;
+    step(sA, sB, sC);
+    if (sB.u < 0) break;
+    step(sB, sC, sA);
+    if (sC.u < 0) break;
+    step(sC, sA, sB);
+  }
+  finish_task();
+  flush_stats(st.stats, c, lane);
+}
+
 // Messages in flight after round r = p.round - 1, as row pushes into next[p.round&1] + T bits
 // (the form k_gossip_update consumes), one wave per receiver u, lane = word, serial over u's
 // slots (not a hot path):
@@ -985,13 +1110,10 @@ __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st,
     return STORE_E ? g.rev[rb + lane] : (uint32_t)g.colidx[rb + lane];
   };
 
-  for (int64_t task = task0 + (int64_t)blockIdx.x * WPB + wib; task < ntasks;
-       task += (int64_t)gridDim.x * WPB) {
-    if (task < nwords && nslices == 1) {
-      // pipelined: row offsets of the 32 peers in one load; the next active peer's frontier
-      // word and receiver slots are in flight while the current one computes
-      uint32_t todo = st.A[cur][task];
-      if (!todo) continue;
+  // one 32-peer bitmap task of single-slice rows (W <= 64), pipelined: row offsets of the
+  // peers by scalar loads; the next active peer's frontier word and receiver slots are in
+  // flight while the current one computes
+  auto bitmap_task = [&](int64_t task, uint32_t todo) {
       const int64_t base = task << 5;
       // row offsets by SCALAR loads (lgkmcnt): a vector load here would make every vertex
       // wait on vmcnt, i.e. on the previous vertex's outstanding row stores
@@ -1030,8 +1152,26 @@ __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st,
         f1 = f2;
         rv1 = rv2;
       }
-      continue;
+  };
+  int64_t first = task0;
+  if (nslices == 1 && task0 < nwords) {
+    // SCAN_W activity words per wave pass (lane = task): the active tasks of a sparse round
+    // are found with one load per lane instead of one dependent load per task
+    const int64_t wave = (int64_t)blockIdx.x * WPB + wib, nwave = (int64_t)gridDim.x * WPB;
+    for (int64_t tb = task0 + wave * SCAN_W; tb < nwords; tb += nwave * SCAN_W) {
+      const int64_t tl = tb + lane;
+      const uint32_t al = lane < SCAN_W && tl < nwords ? st.A[cur][tl] : 0u;
+      uint64_t busy = __ballot(al != 0u);
+      while (busy) {
+        const int l = __builtin_ctzll(busy);
+        busy &= busy - 1ull;
+        bitmap_task(tb + l, (uint32_t)__builtin_amdgcn_readlane((int)al, l));
+      }
     }
+    first = nwords;
+  }
+  for (int64_t task = first + (int64_t)blockIdx.x * WPB + wib; task < ntasks;
+       task += (int64_t)gridDim.x * WPB) {
     auto one_source = [&](int64_t v, int chunk) {
       const int64_t rb = g.rowptr[v];
       const int64_t deg = g.rowptr[v + 1] - rb;
@@ -1748,7 +1888,14 @@ hipError_t launch_materialize(const DevGraph& g, const DevState& st, const Round
 hipError_t launch_gossip_update(const DevGraph& g, const DevState& st, const RoundParams& p,
                                 hipStream_t s) {
   const int grid = grid_tasks((g.V + 31) >> 5);
-  hipLaunchKernelGGL(k_gossip_update, dim3(grid), dim3(256), 0, s, g, st, p);
+  static const bool pipelined = [] {  // P2PG_UPDATE1=0: the unpipelined kernel (A/B only)
+    const char* e = std::getenv("P2PG_UPDATE1");
+    return !(e && std::strcmp(e, "0") == 0);
+  }();
+  if (st.W <= 64 && pipelined)
+    hipLaunchKernelGGL(k_gossip_update1, dim3(grid), dim3(256), 0, s, g, st, p);
+  else
+    hipLaunchKernelGGL(k_gossip_update, dim3(grid), dim3(256), 0, s, g, st, p);
   return hipGetLastError();
 }
 
