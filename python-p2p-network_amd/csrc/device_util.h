@@ -168,6 +168,49 @@ __device__ __forceinline__ int64_t readlane64(int64_t x, int l) {
   return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
+// Lane-varying register read (ds_bpermute).  Every call site runs with the whole wave active:
+// a disabled source lane would not deliver its value.
+__device__ __forceinline__ uint32_t bperm(int src_lane, uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane << 2, (int)x);
+}
+
+__device__ __forceinline__ uint64_t bperm64(int src_lane, uint64_t x) {
+  return ((uint64_t)bperm(src_lane, (uint32_t)(x >> 32)) << 32) | bperm(src_lane, (uint32_t)x);
+}
+
+// Inclusive running maximum over the wave (the DPP steps of wave_scan_u32; 0 is the identity).
+__device__ __forceinline__ uint32_t wave_scan_max_u32(uint32_t x) {
+  auto mx = [](uint32_t a, uint32_t b) { return a > b ? a : b; };
+  x = mx(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false));
+  x = mx(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false));
+  x = mx(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false));
+  x = mx(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false));
+  x = mx(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false));
+  x = mx(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false));
+  return x;
+}
+
+// Position of the n-th (0-based) set bit of x; n < popcount(x).
+__device__ __forceinline__ uint32_t select_bit32(uint32_t x, uint32_t n) {
+  uint32_t pos = 0;
+#pragma unroll
+  for (uint32_t s = 16; s; s >>= 1) {
+    const uint32_t c = (uint32_t)__popc(x & ((1u << s) - 1u));
+    const bool up = n >= c;
+    n = up ? n - c : n;
+    x = up ? x >> s : x;
+    pos = up ? pos + s : pos;
+  }
+  return pos;
+}
+
+__device__ __forceinline__ uint32_t select_bit64(uint64_t x, uint32_t n) {
+  const uint32_t lo = (uint32_t)x;
+  const uint32_t cl = (uint32_t)__popc(lo);
+  const bool up = n >= cl;
+  return (up ? 32u : 0u) + select_bit32(up ? (uint32_t)(x >> 32) : lo, up ? n - cl : n);
+}
+
 // Orders this wave's LDS writes before its later LDS reads by other lanes.
 __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");

@@ -73,6 +73,8 @@ struct p2pg_engine {
                                // rows: word density alone is high whenever anything is active)
   int push_mode = 0;           // 0 auto, 1 always row atomics, 2 always edge stores
   bool fused = true;           // dense rounds after dense rounds: one pull+scatter pass
+  bool sparse_lp = true;       // sparse rounds: lane-parallel scatter (relay_sparse.hip) when
+                               // the rows allow it; P2PG_SPARSE_LP=0 keeps the per-source one
   bool skip_frontier = false;  // p2pg_run, not its last two allowed rounds: fused rounds may skip F
   bool frontier_kept = true;   // F[(round-1)&1] holds the last round's first receipts
   bool frontier_kept_prev = true;  // ... and F[round&1] the round before (delivery parents)
@@ -101,9 +103,19 @@ struct p2pg_engine {
   int32_t arr_round = -1;       // the round whose arrivals travelled on that graph
   bool consume_next = false;    // the next round consumes materialized rows (update kernel)
   uint64_t total_relays = 0;    // relays since the last reset (= sum of message_count_send)
+  // sparse-round scatter (relay_sparse.hip): the (peer, word) list of a frontier; its fill
+  // count lives in the stats buffer, slot STAT_COUNT
+  uint64_t* d_wlist = nullptr;
+  int64_t wlist_cap = 0;
+  uint8_t* d_touched = nullptr;  // one byte per peer (V rounded up to 32), zero between launches
+  bool wlist_check = false;     // a sparse scatter ran this round: check its count after it
 };
 
 namespace {
+
+// stats buffer: STAT_N x STAT_SHARDS round counters, then the sparse scatter's list count
+constexpr int STAT_COUNT = STAT_N * STAT_SHARDS;
+constexpr size_t STAT_BYTES = sizeof(unsigned long long) * (STAT_COUNT + 1);
 
 int fail(p2pg_engine* e, int code, const std::string& msg) {
   if (e) e->err = msg;
@@ -140,6 +152,9 @@ void free_state(p2pg_engine* e) {
   for (int i = 0; i < 2; ++i) dfree(s.E[i]);
   for (int i = 0; i < 2; ++i) dfree(s.AW[i]);
   dfree(s.stats);
+  dfree(e->d_wlist);
+  e->wlist_cap = 0;
+  dfree(e->d_touched);
 #ifdef P2PG_PROF
   if (s.prof) {
     unsigned long long h[16];
@@ -273,6 +288,50 @@ int resolve_timings(p2pg_engine* e) {
   return P2PG_OK;
 }
 
+// Can round p's row-atomic push run lane-parallel (relay_sparse.hip)?
+bool sparse_scatter_on(const p2pg_engine* e) {
+  return e->sparse_lp && gossip_scatter_sparse_supported(e->st);
+}
+
+// Row-atomic push of the frontier of round p.round over g: lane-parallel when the rows allow it
+// (n_words = that frontier's nonzero words, which sizes the (peer, word) list), else per source.
+hipError_t launch_scatter_atomic(p2pg_engine* e, const DevGraph& g, const RoundParams& p,
+                                 uint64_t n_words) {
+  DevState& s = e->st;
+  if (!sparse_scatter_on(e))
+    return launch_gossip_scatter(g, s, p, e->d_hub, e->n_hub, false, e->stream);
+  const int64_t need = (int64_t)n_words > 0 ? (int64_t)n_words : 1;
+  if (need > e->wlist_cap) {
+    dfree(e->d_wlist);
+    e->wlist_cap = 0;
+    const int64_t cap = need + need / 4 + 4096;  // grows by steps, not per round
+    hipError_t r = hipMalloc((void**)&e->d_wlist, sizeof(uint64_t) * (size_t)cap);
+    if (r != hipSuccess) return r;
+    e->wlist_cap = cap;
+  }
+  if (!e->d_touched) {
+    const size_t tb = (size_t)((e->V + 31) >> 5) << 5;
+    hipError_t r = hipMalloc((void**)&e->d_touched, tb ? tb : 32);
+    if (r == hipSuccess) r = hipMemsetAsync(e->d_touched, 0, tb ? tb : 32, e->stream);
+    if (r != hipSuccess) return r;
+  }
+  e->wlist_check = true;
+  return launch_gossip_scatter_sparse(g, s, p, need, e->d_wlist, e->wlist_cap,
+                                      s.stats + STAT_COUNT, e->d_touched, e->stream);
+}
+
+// After the stream synced on a round whose push ran lane-parallel: the list must have held
+// every (peer, word) pair (n_words is the frontier's own count, so a shortfall is a bug).
+int check_scatter_list(p2pg_engine* e, unsigned long long listed) {
+  if (!e->wlist_check) return P2PG_OK;
+  e->wlist_check = false;
+  if ((int64_t)listed > e->wlist_cap)
+    return fail(e, P2PG_ERR_STATE, "sparse scatter: " + std::to_string(listed) +
+                                          " frontier words listed, room for " +
+                                          std::to_string(e->wlist_cap));
+  return P2PG_OK;
+}
+
 // Dense-round edge-mask planes E, sized by the current nnz: one, or two for fused rounds
 // (round r pulls E[(r-1)&1], pushes E[r&1]); only if they fit with headroom -- else gossip
 // pushes by row atomics only.  Replaces any previous planes (their contents are dropped).
@@ -337,7 +396,7 @@ int alloc_state(p2pg_engine* e) {
     if ((rc = A((void**)&s.hop, hb))) return rc;
     if ((rc = A((void**)&s.parent, hb))) return rc;
   }
-  if ((rc = A((void**)&s.stats, sizeof(unsigned long long) * STAT_N * STAT_SHARDS))) return rc;
+  if ((rc = A((void**)&s.stats, STAT_BYTES))) return rc;
 #ifdef P2PG_PROF
   if ((rc = A((void**)&s.prof, sizeof(unsigned long long) * 16))) return rc;
   HIPCHK(e, hipMemset(s.prof, 0, sizeof(unsigned long long) * 16));
@@ -369,6 +428,7 @@ int p2pg_create(const p2pg_config* cfg, p2pg_engine** out) {
   if (const char* t = std::getenv("P2PG_E_THRESH")) e->e_thresh = std::atof(t);
   if (const char* t = std::getenv("P2PG_V_THRESH")) e->v_thresh = std::atof(t);
   if (const char* f = std::getenv("P2PG_FUSED")) e->fused = std::strcmp(f, "0") != 0;
+  if (const char* f = std::getenv("P2PG_SPARSE_LP")) e->sparse_lp = std::strcmp(f, "0") != 0;
   if (const char* m = std::getenv("P2PG_GOSSIP_PUSH"))
     e->push_mode = !std::strcmp(m, "atomic") ? 1 : (!std::strcmp(m, "store") ? 2 : 0);
   HIPCHK(e, hipSetDevice(cfg->device));
@@ -376,8 +436,7 @@ int p2pg_create(const p2pg_config* cfg, p2pg_engine** out) {
   e->stream = e->own_stream;
   HIPCHK(e, hipEventCreate(&e->ev[0]));
   HIPCHK(e, hipEventCreate(&e->ev[1]));
-  HIPCHK(e, hipHostMalloc((void**)&e->h_stats,
-                          sizeof(unsigned long long) * STAT_N * STAT_SHARDS));
+  HIPCHK(e, hipHostMalloc((void**)&e->h_stats, STAT_BYTES));
   *out = e;
   return P2PG_OK;
 }
@@ -594,7 +653,7 @@ int p2pg_step_begin(p2pg_engine* e) {
   if (e->done) return P2PG_OK;
   HIPCHK(e, hipSetDevice(e->cfg.device));
   DevState& s = e->st;
-  HIPCHK(e, hipMemsetAsync(s.stats, 0, sizeof(unsigned long long) * STAT_N * STAT_SHARDS, e->stream));
+  HIPCHK(e, hipMemsetAsync(s.stats, 0, STAT_BYTES, e->stream));
   e->begun = true;
   if (!split_round(e)) return P2PG_OK;
   // phase 0: peers without a ghost neighbour, which need none of the rows still in transit
@@ -694,8 +753,7 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
       return rc;
   uint64_t tot[STAT_N] = {0};
   auto read_stats = [&]() -> int {
-    HIPCHK(e, hipMemcpyAsync(e->h_stats, s.stats, sizeof(unsigned long long) * STAT_N * STAT_SHARDS,
-                             hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipMemcpyAsync(e->h_stats, s.stats, STAT_BYTES, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
     int r2 = resolve_timings(e);
     if (r2) return r2;
@@ -717,24 +775,29 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
   } else if (gossip) {
     // push form for this round's sends: row atomics when the frontier is sparse, whole-row
     // edge-mask stores (+ pull next round) when most words of the active rows are set
-    bool use_e = false;
+    bool use_e = false, have_tot = false;
     if (s.E[0] && !e->d_gid) {  // partitioned gossip pushes by row atomics (ghost rows travel)
       if (e->push_mode == 2) {
         use_e = true;
       } else if (e->push_mode == 0) {
         if ((rc = read_stats())) return rc;
+        have_tot = true;
         use_e = (double)tot[ST_ACTIVE_W] >=
                 e->e_thresh * (double)tot[ST_ACTIVE_V] * (double)e->W && tot[ST_ACTIVE_V] > 0 &&
                 (double)tot[ST_ACTIVE_V] >= e->v_thresh * (double)e->V;
       }
     }
+    // the lane-parallel sparse push sizes its (peer, word) list by the frontier's word count
+    if (!use_e && !have_tot && sparse_scatter_on(e) && (rc = read_stats())) return rc;
     if ((rc = timed(e, use_e ? 6 : 2, [&] {
-           return launch_gossip_scatter(g, s, p, e->d_hub, e->n_hub, use_e, e->stream);
+           return use_e ? launch_gossip_scatter(g, s, p, e->d_hub, e->n_hub, true, e->stream)
+                        : launch_scatter_atomic(e, g, p, tot[ST_ACTIVE_W]);
          })))
       return rc;
     e->last_push_e = use_e;
   }
   if ((rc = read_stats())) return rc;
+  if ((rc = check_scatter_list(e, e->h_stats[STAT_COUNT]))) return rc;
 #ifdef P2PG_PROF
   if (fused_round && s.prof && std::getenv("P2PG_PROF_ROUNDS")) {
     // development builds: per-round fused-kernel segment clocks (then reset)
@@ -1143,10 +1206,15 @@ int p2pg_update_edges(p2pg_engine* e, int64_t n_add, const int32_t* add, int64_t
       HIPCHK(e, hipMemsetAsync(s.next[nx], 0, e->plane_bytes, e->stream));
       HIPCHK(e, hipMemsetAsync(s.T[nx], 0, e->bm_bytes, e->stream));
       p.round = e->round - 1;
-      lr = launch_gossip_scatter(gold, s, p, e->d_hub, e->n_hub, false, e->stream);
+      lr = launch_scatter_atomic(e, gold, p, e->prev_aw);
       if (lr != hipSuccess) return fail(e, P2PG_ERR_HIP, std::string("update_edges: ") + hipGetErrorString(lr));
     }
     HIPCHK(e, hipStreamSynchronize(e->stream));
+    if (e->wlist_check) {
+      unsigned long long listed = 0;
+      HIPCHK(e, hipMemcpy(&listed, s.stats + STAT_COUNT, sizeof(listed), hipMemcpyDeviceToHost));
+      if (int rc2 = check_scatter_list(e, listed)) return rc2;
+    }
     e->consume_next = true;
     e->last_push_e = false;
     // keep the old rows for the parents of the receiving round (record / deliveries)

@@ -46,16 +46,6 @@ struct GroupedLds {
   uint8_t owner[64];                   // pick-window slot -> batch peer
 };
 
-// Lane-varying register read (ds_bpermute).  Every call site runs with the whole wave active:
-// a disabled source lane would not deliver its value.
-__device__ __forceinline__ uint32_t bperm(int src_lane, uint32_t x) {
-  return (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane << 2, (int)x);
-}
-
-__device__ __forceinline__ uint64_t bperm64(int src_lane, uint64_t x) {
-  return ((uint64_t)bperm(src_lane, (uint32_t)(x >> 32)) << 32) | bperm(src_lane, (uint32_t)x);
-}
-
 // lane-varying read of lane src's 64-bit value
 __device__ __forceinline__ int64_t readlane64_v(int64_t x, int src_lane) {
   return (int64_t)bperm64(src_lane, (uint64_t)x);

@@ -1,0 +1,273 @@
+// Gossip sparse rounds: the row-atomic push of a round's first receipts, lane-parallel.
+//
+// Why: in a sparse round (few active words per active peer: config 4's rounds 0-8 and 26-45
+// carry 1-2 new bits per active peer) the per-source scatter of relay_kernels.hip
+// (k_gossip_scatter<.., false>: one wave per source, lane = word, LDS mask table, flush per
+// neighbour chunk) spends a whole wave visit -- compaction scan, table clear, one pick batch,
+// flush loop -- on one or two bits.  Here the three levels of a push are flattened onto lanes:
+//   level 1  lane = active peer u     (64 tasks of the A bitmap per wave pass, compacted):
+//            the active-word mask AW[u] (W <= 8: the nonzero words of the row);
+//   level 2  its (u, w) pairs are appended to a list (k_sparse_words) ...
+//   level 3  ... which k_sparse_push hands out 64 words per wave pass (a hub's words spread over
+//            many waves; one wave per 64 peers left the hub tasks' wave 10x behind), lane =
+//            (u, w, bit b): Philox + Floyd picks of message w*64+b (gossip_picks_t),
+//            then, per distinct (u, w, target): one atomicOr of the merged mask into
+//            next[target][w] and a byte store into the target's touched byte (the same pushes,
+//            and the same count of distinct (sender, target, word) masks, as the per-source
+//            kernel); k_touched_bits folds the bytes into the T bitmap.
+// Each level's entries are handed out 64 at a time; the owner lane of an entry is found by a
+// marker + running-max scan and its index inside the owner by select-nth-bit, so no per-bit
+// loop runs on one lane.  Level-3 passes never split a word's bits (at most 64), so a mask is
+// merged and counted once.  Reference semantics: Node.send_to_nodes -> send_to_node per chosen
+// connection (node.py:106-120), counted before sending; lost sends (churn, a connection removed
+// by a topology update) push nothing (nodeconnection.py:123-126).
+#include "device_util.h"
+
+namespace p2pg {
+namespace {
+
+template <int KP>
+struct SparseLds {
+  uint32_t own[64];     // owner markers of the current pass
+  uint32_t bit[64];     // level-3 entry -> its message bit
+  uint32_t pk[KP][64];  // level-3 entry -> its picks (slot offsets in the sender's row)
+};
+
+// Owner lane of entry pb + lane of a pass over per-lane ranges [pos, pos + cnt) (pos is the
+// exclusive prefix sum of cnt): every range that meets the pass marks its first slot, and a
+// running maximum fills the rest.  Whole wave active.
+__device__ __forceinline__ int pass_owner(uint32_t* own, int lane, uint32_t pos, uint32_t cnt,
+                                          uint32_t pb) {
+  own[lane] = 0u;
+  wave_lds_sync();
+  if (cnt && pos + cnt > pb && pos < pb + 64u) own[pos > pb ? pos - pb : 0u] = (uint32_t)lane;
+  wave_lds_sync();
+  return (int)wave_scan_max_u32(own[lane]);
+}
+
+// Levels 1-2: the (active peer, active word) pairs of round r's frontier, appended to `list`
+// as u << 6 | w (one atomicAdd per 64 peers).  Grid-stride over 64 task words per wave pass.
+__global__ __launch_bounds__(256) void k_sparse_words(DevGraph g, DevState st, RoundParams p,
+                                                      uint64_t* __restrict__ list, int64_t cap,
+                                                      unsigned long long* __restrict__ count) {
+  __shared__ uint32_t own_all[WPB][64];
+  const int lane = threadIdx.x & 63;
+  const int wib = wave_in_block();
+  uint32_t* own = own_all[wib];
+  const int64_t V = g.V;
+  const int W = st.W;
+  const int cur = p.round & 1;
+  const uint64_t* __restrict__ Fc = st.F[cur];
+  const uint64_t* __restrict__ AWc = st.AW[cur];
+  const uint32_t* __restrict__ Ac = st.A[cur];
+  const int64_t ntasks = (V + 31) >> 5;
+  for (int64_t tb = ((int64_t)blockIdx.x * WPB + wib) * 64; tb < ntasks;
+       tb += (int64_t)gridDim.x * WPB * 64) {
+    const int64_t tl = tb + lane;
+    const uint32_t al = tl < ntasks ? Ac[tl] : 0u;
+    if (!__ballot(al != 0u)) continue;
+    const uint32_t pc = (uint32_t)__popc(al);
+    const uint32_t pinc = wave_scan_u32(pc);
+    const uint32_t pos = pinc - pc;
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)pinc, 63);
+    for (uint32_t pb = 0; pb < total; pb += 64) {
+      // lane = active peer pb + lane of these 64 tasks
+      const int ow = pass_owner(own, lane, pos, pc, pb);
+      const uint32_t opos = bperm(ow, pos), oal = bperm(ow, al);
+      int64_t u = 0;
+      uint64_t am = 0;
+      if (pb + (uint32_t)lane < total) {
+        u = ((tb + ow) << 5) + select_bit32(oal, pb + (uint32_t)lane - opos);
+        if (AWc) {
+          am = AWc[u];
+        } else {  // W <= PACK_W_MAX_PLAIN: the nonzero words of the row
+          for (int w = 0; w < W; ++w) am |= (uint64_t)(Fc[u * W + w] != 0ull) << w;
+        }
+      }
+      const uint32_t wc = (uint32_t)__popcll(am);
+      const uint32_t winc = wave_scan_u32(wc);
+      const uint32_t wtot = (uint32_t)__builtin_amdgcn_readlane((int)winc, 63);
+      uint64_t base = 0;
+      if (lane == 0) base = atomicAdd(count, (unsigned long long)wtot);
+      base = (uint64_t)readlane64((int64_t)base, 0);
+      uint64_t idx = base + winc - wc;
+      for (uint64_t h = am; h; h &= h - 1ull, ++idx)
+        if (idx < (uint64_t)cap) list[idx] = ((uint64_t)u << 6) | (uint64_t)__builtin_ctzll(h);
+    }
+  }
+}
+
+// Level 3: lane = (peer, word, bit) of the listed words, 64 words per wave pass (balanced: a
+// hub's words spread over many waves).  A bit pass [b0, b1) holds whole words only.
+template <bool CHURN, int K>
+__global__ __launch_bounds__(256) void k_sparse_push(DevGraph g, DevState st, RoundParams p,
+                                                     const uint64_t* __restrict__ list,
+                                                     int64_t cap,
+                                                     const unsigned long long* __restrict__ count,
+                                                     uint8_t* __restrict__ touched) {
+  constexpr int KP = K > 0 ? K : 16;
+  __shared__ SparseLds<KP> lds[WPB];
+  const int lane = threadIdx.x & 63;
+  const int wib = wave_in_block();
+  SparseLds<KP>& L = lds[wib];
+  const int W = st.W;
+  const int cur = p.round & 1, nxt = cur ^ 1;
+  const uint64_t* __restrict__ Fc = st.F[cur];
+  uint64_t* __restrict__ nx = st.next[nxt];
+  const uint32_t k = K > 0 ? (uint32_t)K : (uint32_t)p.fanout;
+  const int64_t listed = (int64_t)ldc(count);
+  const int64_t n = listed < cap ? listed : cap;
+  uint64_t pushed = 0;  // distinct (sender, target, word) masks pushed by this lane
+
+  for (int64_t e0 = ((int64_t)blockIdx.x * WPB + wib) * 64; e0 < n;
+       e0 += (int64_t)gridDim.x * WPB * 64) {
+    uint32_t w = 0, deg = 0;
+    int64_t u = 0, rb = 0;
+    uint64_t f = 0;
+    if (e0 + lane < n) {
+      const uint64_t x = list[e0 + lane];
+      u = (int64_t)(x >> 6);
+      w = (uint32_t)(x & 63u);
+      rb = g.rowptr[u];
+      deg = (uint32_t)(g.rowptr[u + 1] - rb);
+      f = Fc[u * W + w];
+    }
+    const uint32_t bc = (uint32_t)__popcll(f);
+    const uint32_t binc = wave_scan_u32(bc);
+    const uint32_t bpos = binc - bc;
+    const uint32_t btot = (uint32_t)__builtin_amdgcn_readlane((int)binc, 63);
+    for (uint32_t b0 = 0; b0 < btot;) {
+      const uint64_t over = __ballot(bc != 0u && bpos >= b0 && bpos + bc > b0 + 64u);
+      const uint32_t b1 =
+          over ? (uint32_t)__builtin_amdgcn_readlane((int)bpos, (int)__builtin_ctzll(over)) : btot;
+      const int bw = pass_owner(L.own, lane, bpos, bc, b0);
+      const uint32_t gpos = bperm(bw, bpos), gcnt = bperm(bw, bc);
+      const uint64_t gf = bperm64(bw, f);
+      const uint32_t gw = bperm(bw, w), gdeg = bperm(bw, deg);
+      const int64_t gu = (int64_t)bperm64(bw, (uint64_t)u);
+      const int64_t grb = (int64_t)bperm64(bw, (uint64_t)rb);
+      const bool bv = (uint32_t)lane < b1 - b0;
+      const uint32_t gs = gpos - b0, ge = gs + gcnt;  // this word's entries [gs, ge)
+      uint32_t b = 0, gv = 0;
+      if (bv) {
+        b = select_bit64(gf, b0 + (uint32_t)lane - gpos);
+        gv = gidx(g, gu);
+        L.bit[lane] = b;
+        if (gdeg > k) {
+          const uint32_t mg = p.msg_base + gw * 64u + b;
+          if constexpr (K > 0) {
+            uint32_t pk[K];
+            gossip_picks_t<K>((uint32_t)p.round, gv, mg, gdeg, p.gseed_lo, p.gseed_hi, pk);
+#pragma unroll
+            for (int q = 0; q < K; ++q) L.pk[q][lane] = pk[q];
+          } else {
+            uint32_t pk[16];
+            gossip_picks((uint32_t)p.round, gv, mg, gdeg, (int)k, p.gseed_lo, p.gseed_hi, pk);
+            for (uint32_t q = 0; q < k; ++q) L.pk[q][lane] = pk[q];
+          }
+        }
+      }
+      wave_lds_sync();
+      if (bv) {
+        const bool all = gdeg <= k;  // every connection, the whole word at once
+        const uint32_t kk = all ? gdeg : k;
+        for (uint32_t q = 0; q < kk; ++q) {
+          uint32_t t;
+          uint64_t mask;
+          if (all) {
+            if ((uint32_t)lane != gs) break;
+            t = q;
+            mask = gf;
+          } else {
+            t = L.pk[q][lane];
+            // first entry of this word to pick t?  Then it pushes the word's merged mask.
+            bool lead = true;
+            for (uint32_t i = gs; i < (uint32_t)lane && lead; ++i)
+              for (uint32_t q2 = 0; q2 < k; ++q2) lead &= L.pk[q2][i] != t;
+            if (!lead) continue;
+            mask = 1ull << b;
+            for (uint32_t i = (uint32_t)lane + 1u; i < ge; ++i) {
+              bool hit = false;
+              for (uint32_t q2 = 0; q2 < k; ++q2) hit |= L.pk[q2][i] == t;
+              if (hit) mask |= 1ull << L.bit[i];
+            }
+          }
+          const int64_t slot = grb + (int64_t)t;
+          if (g.gone && g.gone[slot]) continue;  // connection removed: the push is lost
+          const int32_t v = g.colidx[slot];
+          if (CHURN && churn_dropped((uint32_t)p.round, gv, gidx(g, v), p.churn_thr, p.cseed_lo,
+                                     p.cseed_hi))
+            continue;
+          atomicOr((unsigned long long*)&nx[(int64_t)v * W + gw], (unsigned long long)mask);
+          touched[v] = 1u;  // a plain byte store: a T-bitmap atomic here doubled the atomics
+          pushed += 1;
+        }
+      }
+      wave_lds_sync();  // the entries' LDS is rewritten by the next pass
+      b0 = b1;
+    }
+  }
+  uint64_t c[STAT_N] = {0, 0, 0, 0, 0, 0, 0, 0};
+  c[ST_SCATTER] = pushed;
+  flush_stats(st.stats, c, lane);
+}
+
+// The touched bytes of k_sparse_push -> T bits of round r+1 (one lane per 32-peer task word,
+// the only writer of that word here), bytes cleared for the next sparse round.
+__global__ __launch_bounds__(256) void k_touched_bits(int64_t V, uint32_t* __restrict__ T,
+                                                      uint8_t* __restrict__ touched) {
+  const int64_t ntasks = (V + 31) >> 5;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < ntasks;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    uint4* q = reinterpret_cast<uint4*>(touched + (t << 5));  // V is padded to 32 peers
+    const uint4 a = q[0], b = q[1];
+    const uint32_t wv[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    uint32_t m = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) m |= ((wv[i] >> (8 * j)) & 1u) << (4 * i + j);
+    if (m) {
+      T[t] |= m;
+      q[0] = make_uint4(0u, 0u, 0u, 0u);
+      q[1] = make_uint4(0u, 0u, 0u, 0u);
+    }
+  }
+}
+
+}  // namespace
+
+bool gossip_scatter_sparse_supported(const DevState& st) {
+  return st.W >= 1 && st.W <= 64 && (st.AW[0] != nullptr || st.W <= PACK_W_MAX_PLAIN);
+}
+
+hipError_t launch_gossip_scatter_sparse(const DevGraph& g, const DevState& st,
+                                        const RoundParams& p, int64_t expect, uint64_t* list,
+                                        int64_t cap, unsigned long long* count,
+                                        uint8_t* touched, hipStream_t s) {
+  if (!gossip_scatter_sparse_supported(st) || cap < 1) return hipErrorInvalidValue;
+  hipError_t r = hipMemsetAsync(count, 0, sizeof(unsigned long long), s);
+  if (r != hipSuccess) return r;
+  const int64_t chunks = (((g.V + 31) >> 5) + 63) >> 6;  // 64 task words per wave pass
+  hipLaunchKernelGGL(k_sparse_words, dim3(grid_tasks(chunks)), dim3(256), 0, s, g, st, p, list,
+                     cap, count);
+  const int grid = grid_tasks((expect + 63) >> 6);  // 64 listed words per wave pass
+  const bool ch = p.churn_thr != 0;
+#define P2PG_SPARSE(CH, KK)                                                              \
+  hipLaunchKernelGGL((k_sparse_push<CH, KK>), dim3(grid), dim3(256), 0, s, g, st, p, list, \
+                     cap, count, touched)
+  switch (p.fanout) {
+    case 1: if (ch) P2PG_SPARSE(true, 1); else P2PG_SPARSE(false, 1); break;
+    case 2: if (ch) P2PG_SPARSE(true, 2); else P2PG_SPARSE(false, 2); break;
+    case 3: if (ch) P2PG_SPARSE(true, 3); else P2PG_SPARSE(false, 3); break;
+    case 4: if (ch) P2PG_SPARSE(true, 4); else P2PG_SPARSE(false, 4); break;
+    default: if (ch) P2PG_SPARSE(true, 0); else P2PG_SPARSE(false, 0); break;
+  }
+#undef P2PG_SPARSE
+  const int64_t ntasks = (g.V + 31) >> 5;
+  hipLaunchKernelGGL(k_touched_bits, dim3((unsigned)std::min<int64_t>((ntasks + 255) / 256, 4096)),
+                     dim3(256), 0, s, g.V, st.T[(p.round & 1) ^ 1], touched);
+  return hipGetLastError();
+}
+
+}  // namespace p2pg
