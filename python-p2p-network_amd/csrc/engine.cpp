@@ -108,6 +108,8 @@ struct p2pg_engine {
   uint64_t* d_wlist = nullptr;
   int64_t wlist_cap = 0;
   uint8_t* d_touched = nullptr;  // one byte per peer (V rounded up to 32), zero between launches
+  uint32_t* d_chunk_cnt = nullptr;  // per list chunk: pairs, and their offsets
+  uint64_t* d_chunk_off = nullptr;
   bool wlist_check = false;     // a sparse scatter ran this round: check its count after it
 };
 
@@ -155,6 +157,8 @@ void free_state(p2pg_engine* e) {
   dfree(e->d_wlist);
   e->wlist_cap = 0;
   dfree(e->d_touched);
+  dfree(e->d_chunk_cnt);
+  dfree(e->d_chunk_off);
 #ifdef P2PG_PROF
   if (s.prof) {
     unsigned long long h[16];
@@ -311,13 +315,17 @@ hipError_t launch_scatter_atomic(p2pg_engine* e, const DevGraph& g, const RoundP
   }
   if (!e->d_touched) {
     const size_t tb = (size_t)((e->V + 31) >> 5) << 5;
+    const size_t nc = ((size_t)sparse_chunks(e->V) + 8) & ~(size_t)7;  // 16 B loads
     hipError_t r = hipMalloc((void**)&e->d_touched, tb ? tb : 32);
     if (r == hipSuccess) r = hipMemsetAsync(e->d_touched, 0, tb ? tb : 32, e->stream);
+    if (r == hipSuccess) r = hipMalloc((void**)&e->d_chunk_cnt, sizeof(uint32_t) * nc);
+    if (r == hipSuccess) r = hipMalloc((void**)&e->d_chunk_off, sizeof(uint64_t) * nc);
     if (r != hipSuccess) return r;
   }
   e->wlist_check = true;
-  return launch_gossip_scatter_sparse(g, s, p, need, e->d_wlist, e->wlist_cap,
-                                      s.stats + STAT_COUNT, e->d_touched, e->stream);
+  const SparseBufs b{e->d_wlist, e->wlist_cap, s.stats + STAT_COUNT, e->d_chunk_cnt,
+                     e->d_chunk_off, e->d_touched};
+  return launch_gossip_scatter_sparse(g, s, p, need, b, e->stream);
 }
 
 // After the stream synced on a round whose push ran lane-parallel: the list must have held

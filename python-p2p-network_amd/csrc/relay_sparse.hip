@@ -7,7 +7,7 @@
 // flush loop -- on one or two bits.  Here the three levels of a push are flattened onto lanes:
 //   level 1  lane = active peer u     (64 tasks of the A bitmap per wave pass, compacted):
 //            the active-word mask AW[u] (W <= 8: the nonzero words of the row);
-//   level 2  its (u, w) pairs are appended to a list (k_sparse_words) ...
+//   level 2  its (u, w) pairs are listed in peer order (k_sparse_words, two passes) ...
 //   level 3  ... which k_sparse_push hands out 64 words per wave pass (a hub's words spread over
 //            many waves; one wave per 64 peers left the hub tasks' wave 10x behind), lane =
 //            (u, w, bit b): Philox + Floyd picks of message w*64+b (gossip_picks_t),
@@ -45,11 +45,21 @@ __device__ __forceinline__ int pass_owner(uint32_t* own, int lane, uint32_t pos,
   return (int)wave_scan_max_u32(own[lane]);
 }
 
-// Levels 1-2: the (active peer, active word) pairs of round r's frontier, appended to `list`
-// as u << 6 | w (one atomicAdd per 64 peers).  Grid-stride over 64 task words per wave pass.
+// Levels 1-2: the (active peer, active word) pairs of round r's frontier, listed as u << 6 | w
+// in peer order, without atomics: pass COUNT counts each chunk's pairs (SW_TASKS task words per
+// chunk), k_chunk_scan turns the counts into offsets, pass WRITE stores the pairs there, 64 per
+// store instruction (lane = pair: owner peer by pass_owner, word by select-nth-bit).  A single
+// list counter took one same-address atomic per 64 peers: ~8 ns each, serialized (0.1-1.2 ms
+// per round).  Chunks are small because the Barabasi-Albert hubs (lowest ids, most active
+// words) share the first tasks.
+#ifndef P2PG_SW_TASKS
+#define P2PG_SW_TASKS 16
+#endif
+constexpr int SW_TASKS = P2PG_SW_TASKS;
+
+template <bool WRITE>
 __global__ __launch_bounds__(256) void k_sparse_words(DevGraph g, DevState st, RoundParams p,
-                                                      uint64_t* __restrict__ list, int64_t cap,
-                                                      unsigned long long* __restrict__ count) {
+                                                      SparseBufs b) {
   __shared__ uint32_t own_all[WPB][64];
   const int lane = threadIdx.x & 63;
   const int wib = wave_in_block();
@@ -61,17 +71,23 @@ __global__ __launch_bounds__(256) void k_sparse_words(DevGraph g, DevState st, R
   const uint64_t* __restrict__ AWc = st.AW[cur];
   const uint32_t* __restrict__ Ac = st.A[cur];
   const int64_t ntasks = (V + 31) >> 5;
-  for (int64_t tb = ((int64_t)blockIdx.x * WPB + wib) * 64; tb < ntasks;
-       tb += (int64_t)gridDim.x * WPB * 64) {
+  for (int64_t tb = ((int64_t)blockIdx.x * WPB + wib) * SW_TASKS; tb < ntasks;
+       tb += (int64_t)gridDim.x * WPB * SW_TASKS) {
+    const int64_t chunk = tb / SW_TASKS;
     const int64_t tl = tb + lane;
-    const uint32_t al = tl < ntasks ? Ac[tl] : 0u;
-    if (!__ballot(al != 0u)) continue;
+    const uint32_t al = lane < SW_TASKS && tl < ntasks ? Ac[tl] : 0u;
+    if (!__ballot(al != 0u)) {
+      if (!WRITE && lane == 0) b.chunk_cnt[chunk] = 0u;
+      continue;
+    }
     const uint32_t pc = (uint32_t)__popc(al);
     const uint32_t pinc = wave_scan_u32(pc);
     const uint32_t pos = pinc - pc;
     const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)pinc, 63);
+    uint64_t base = WRITE ? b.chunk_off[chunk] : 0ull;  // wave-uniform
+    uint32_t nwords = 0;
     for (uint32_t pb = 0; pb < total; pb += 64) {
-      // lane = active peer pb + lane of these 64 tasks
+      // lane = active peer pb + lane of this chunk
       const int ow = pass_owner(own, lane, pos, pc, pb);
       const uint32_t opos = bperm(ow, pos), oal = bperm(ow, al);
       int64_t u = 0;
@@ -86,25 +102,80 @@ __global__ __launch_bounds__(256) void k_sparse_words(DevGraph g, DevState st, R
       }
       const uint32_t wc = (uint32_t)__popcll(am);
       const uint32_t winc = wave_scan_u32(wc);
+      const uint32_t wpos = winc - wc;
       const uint32_t wtot = (uint32_t)__builtin_amdgcn_readlane((int)winc, 63);
-      uint64_t base = 0;
-      if (lane == 0) base = atomicAdd(count, (unsigned long long)wtot);
-      base = (uint64_t)readlane64((int64_t)base, 0);
-      uint64_t idx = base + winc - wc;
-      for (uint64_t h = am; h; h &= h - 1ull, ++idx)
-        if (idx < (uint64_t)cap) list[idx] = ((uint64_t)u << 6) | (uint64_t)__builtin_ctzll(h);
+      nwords += wtot;
+      if (WRITE) {
+        // lane = pair wb + lane of these peers
+        for (uint32_t wb = 0; wb < wtot; wb += 64) {
+          const int pw = pass_owner(own, lane, wpos, wc, wb);
+          const uint32_t ppos = bperm(pw, wpos);
+          const uint64_t pam = bperm64(pw, am);
+          const uint64_t pu = bperm64(pw, (uint64_t)u);
+          const uint64_t idx = base + wb + (uint64_t)lane;
+          if (wb + (uint32_t)lane < wtot && idx < (uint64_t)b.cap)
+            b.list[idx] = (pu << 6) | select_bit64(pam, wb + (uint32_t)lane - ppos);
+        }
+        base += wtot;
+      }
     }
+    if (!WRITE && lane == 0) b.chunk_cnt[chunk] = nwords;
   }
+}
+
+// Exclusive prefix sum of the chunk counts (one block): chunk_off, and the total into *count.
+// Tiles of 1024 x 8 counts: a thread's 8 consecutive counts arrive in two 16 B loads, so a
+// tile costs one memory trip (a per-thread serial range cost ~20 trips: 26 us per launch).
+__global__ __launch_bounds__(1024) void k_chunk_scan(int64_t n, SparseBufs b) {
+  __shared__ uint64_t wsum[16];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  uint64_t carry = 0;
+  for (int64_t tile = 0; tile < n; tile += 8192) {
+    const int64_t i0 = tile + 8 * (int64_t)t;
+    uint32_t c[8];
+    if (i0 + 8 <= n) {  // chunk_cnt is 16 B aligned
+      const uint4 a = *reinterpret_cast<const uint4*>(b.chunk_cnt + i0);
+      const uint4 d = *reinterpret_cast<const uint4*>(b.chunk_cnt + i0 + 4);
+      c[0] = a.x; c[1] = a.y; c[2] = a.z; c[3] = a.w;
+      c[4] = d.x; c[5] = d.y; c[6] = d.z; c[7] = d.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) c[j] = i0 + j < n ? b.chunk_cnt[i0 + j] : 0u;
+    }
+    uint64_t s = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += c[j];
+    // block exclusive scan of s: wave scans (64-bit shuffles), then the 16 wave totals
+    uint64_t x = s;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint64_t y = __shfl_up(x, o);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wv] = x;
+    __syncthreads();
+    uint64_t before = carry, all = carry;
+    for (int i = 0; i < 16; ++i) {
+      if (i < wv) before += wsum[i];
+      all += wsum[i];
+    }
+    __syncthreads();  // wsum is rewritten by the next tile
+    uint64_t run = before + x - s;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (i0 + j < n) b.chunk_off[i0 + j] = run;
+      run += c[j];
+    }
+    carry = all;
+  }
+  if (t == 0) *b.count = (unsigned long long)carry;
 }
 
 // Level 3: lane = (peer, word, bit) of the listed words, 64 words per wave pass (balanced: a
 // hub's words spread over many waves).  A bit pass [b0, b1) holds whole words only.
 template <bool CHURN, int K>
 __global__ __launch_bounds__(256) void k_sparse_push(DevGraph g, DevState st, RoundParams p,
-                                                     const uint64_t* __restrict__ list,
-                                                     int64_t cap,
-                                                     const unsigned long long* __restrict__ count,
-                                                     uint8_t* __restrict__ touched) {
+                                                     SparseBufs sb) {
   constexpr int KP = K > 0 ? K : 16;
   __shared__ SparseLds<KP> lds[WPB];
   const int lane = threadIdx.x & 63;
@@ -115,8 +186,10 @@ __global__ __launch_bounds__(256) void k_sparse_push(DevGraph g, DevState st, Ro
   const uint64_t* __restrict__ Fc = st.F[cur];
   uint64_t* __restrict__ nx = st.next[nxt];
   const uint32_t k = K > 0 ? (uint32_t)K : (uint32_t)p.fanout;
-  const int64_t listed = (int64_t)ldc(count);
-  const int64_t n = listed < cap ? listed : cap;
+  const uint64_t* __restrict__ list = sb.list;
+  uint8_t* __restrict__ touched = sb.touched;
+  const int64_t listed = (int64_t)ldc(sb.count);
+  const int64_t n = listed < sb.cap ? listed : sb.cap;
   uint64_t pushed = 0;  // distinct (sender, target, word) masks pushed by this lane
 
   for (int64_t e0 = ((int64_t)blockIdx.x * WPB + wib) * 64; e0 < n;
@@ -241,21 +314,21 @@ bool gossip_scatter_sparse_supported(const DevState& st) {
   return st.W >= 1 && st.W <= 64 && (st.AW[0] != nullptr || st.W <= PACK_W_MAX_PLAIN);
 }
 
+int64_t sparse_chunks(int64_t V) { return (((V + 31) >> 5) + SW_TASKS - 1) / SW_TASKS; }
+
 hipError_t launch_gossip_scatter_sparse(const DevGraph& g, const DevState& st,
-                                        const RoundParams& p, int64_t expect, uint64_t* list,
-                                        int64_t cap, unsigned long long* count,
-                                        uint8_t* touched, hipStream_t s) {
-  if (!gossip_scatter_sparse_supported(st) || cap < 1) return hipErrorInvalidValue;
-  hipError_t r = hipMemsetAsync(count, 0, sizeof(unsigned long long), s);
-  if (r != hipSuccess) return r;
-  const int64_t chunks = (((g.V + 31) >> 5) + 63) >> 6;  // 64 task words per wave pass
-  hipLaunchKernelGGL(k_sparse_words, dim3(grid_tasks(chunks)), dim3(256), 0, s, g, st, p, list,
-                     cap, count);
+                                        const RoundParams& p, int64_t expect,
+                                        const SparseBufs& b, hipStream_t s) {
+  if (!gossip_scatter_sparse_supported(st) || b.cap < 1) return hipErrorInvalidValue;
+  const int64_t chunks = sparse_chunks(g.V);
+  const int wgrid = grid_tasks(chunks);
+  hipLaunchKernelGGL(k_sparse_words<false>, dim3(wgrid), dim3(256), 0, s, g, st, p, b);
+  hipLaunchKernelGGL(k_chunk_scan, dim3(1), dim3(1024), 0, s, chunks, b);
+  hipLaunchKernelGGL(k_sparse_words<true>, dim3(wgrid), dim3(256), 0, s, g, st, p, b);
   const int grid = grid_tasks((expect + 63) >> 6);  // 64 listed words per wave pass
   const bool ch = p.churn_thr != 0;
-#define P2PG_SPARSE(CH, KK)                                                              \
-  hipLaunchKernelGGL((k_sparse_push<CH, KK>), dim3(grid), dim3(256), 0, s, g, st, p, list, \
-                     cap, count, touched)
+#define P2PG_SPARSE(CH, KK) \
+  hipLaunchKernelGGL((k_sparse_push<CH, KK>), dim3(grid), dim3(256), 0, s, g, st, p, b)
   switch (p.fanout) {
     case 1: if (ch) P2PG_SPARSE(true, 1); else P2PG_SPARSE(false, 1); break;
     case 2: if (ch) P2PG_SPARSE(true, 2); else P2PG_SPARSE(false, 2); break;
@@ -266,7 +339,7 @@ hipError_t launch_gossip_scatter_sparse(const DevGraph& g, const DevState& st,
 #undef P2PG_SPARSE
   const int64_t ntasks = (g.V + 31) >> 5;
   hipLaunchKernelGGL(k_touched_bits, dim3((unsigned)std::min<int64_t>((ntasks + 255) / 256, 4096)),
-                     dim3(256), 0, s, g.V, st.T[(p.round & 1) ^ 1], touched);
+                     dim3(256), 0, s, g.V, st.T[(p.round & 1) ^ 1], b.touched);
   return hipGetLastError();
 }
 
