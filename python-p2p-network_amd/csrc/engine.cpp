@@ -44,6 +44,8 @@ struct p2pg_engine {
   int64_t n_hub = 0;
   int64_t* d_hub_big = nullptr;  // the chunk items of sources with deg > HUB_T (fused rounds)
   int64_t n_hub_big = 0;
+  int32_t* d_wide_big = nullptr;  // sources with deg > HUB_T (fused rounds' hub pushes)
+  int64_t n_wide_big = 0;
   uint32_t* d_rev = nullptr;   // gossip: reverse edge slots
   // pull hub split (deg > HUB_T)
   uint32_t* d_H = nullptr;
@@ -73,6 +75,8 @@ struct p2pg_engine {
                                // rows: word density alone is high whenever anything is active)
   int push_mode = 0;           // 0 auto, 1 always row atomics, 2 always edge stores
   bool fused = true;           // dense rounds after dense rounds: one pull+scatter pass
+  bool wide_atomic = true;     // fused rounds: hub pushes by atomics (P2PG_WIDE_ATOMIC=0: one
+                               // wave per 16-connection chunk item)
   bool sparse_lp = true;       // sparse rounds: lane-parallel scatter (relay_sparse.hip) when
                                // the rows allow it; P2PG_SPARSE_LP=0 keeps the per-source one
   bool skip_frontier = false;  // p2pg_run, not its last two allowed rounds: fused rounds may skip F
@@ -187,6 +191,7 @@ void free_topology(p2pg_engine* e) {
   dfree(e->d_colidx);
   dfree(e->d_hub);
   dfree(e->d_hub_big);
+  dfree(e->d_wide_big);
   dfree(e->d_rev);
   dfree(e->d_H);
   dfree(e->d_hub_items);
@@ -196,6 +201,7 @@ void free_topology(p2pg_engine* e) {
   e->hp = HubPlan{};
   e->n_hub = 0;
   e->n_hub_big = 0;
+  e->n_wide_big = 0;
 }
 
 void free_graph(p2pg_engine* e) {
@@ -204,6 +210,7 @@ void free_graph(p2pg_engine* e) {
   dfree(e->d_colidx);
   dfree(e->d_hub);
   dfree(e->d_hub_big);
+  dfree(e->d_wide_big);
   dfree(e->d_rev);
   dfree(e->d_H);
   dfree(e->d_hub_items);
@@ -226,6 +233,7 @@ void free_graph(p2pg_engine* e) {
   e->hp = HubPlan{};
   e->n_hub = 0;
   e->n_hub_big = 0;
+  e->n_wide_big = 0;
 }
 
 RoundParams params(const p2pg_engine* e) {
@@ -297,14 +305,11 @@ bool sparse_scatter_on(const p2pg_engine* e) {
   return e->sparse_lp && gossip_scatter_sparse_supported(e->st);
 }
 
-// Row-atomic push of the frontier of round p.round over g: lane-parallel when the rows allow it
-// (n_words = that frontier's nonzero words, which sizes the (peer, word) list), else per source.
-hipError_t launch_scatter_atomic(p2pg_engine* e, const DevGraph& g, const RoundParams& p,
-                                 uint64_t n_words) {
-  DevState& s = e->st;
-  if (!sparse_scatter_on(e))
-    return launch_gossip_scatter(g, s, p, e->d_hub, e->n_hub, false, e->stream);
-  const int64_t need = (int64_t)n_words > 0 ? (int64_t)n_words : 1;
+// Buffers of the lane-parallel pushes, grown on demand: a (peer, word) list of >= need entries,
+// its chunk counts / offsets, the touched bytes.  Its fill count goes to the stats slot
+// STAT_COUNT and is checked after the round (check_scatter_list).
+hipError_t sparse_bufs(p2pg_engine* e, int64_t need, SparseBufs& b) {
+  need = need > 0 ? need : 1;
   if (need > e->wlist_cap) {
     dfree(e->d_wlist);
     e->wlist_cap = 0;
@@ -323,9 +328,27 @@ hipError_t launch_scatter_atomic(p2pg_engine* e, const DevGraph& g, const RoundP
     if (r != hipSuccess) return r;
   }
   e->wlist_check = true;
-  const SparseBufs b{e->d_wlist, e->wlist_cap, s.stats + STAT_COUNT, e->d_chunk_cnt,
-                     e->d_chunk_off, e->d_touched};
-  return launch_gossip_scatter_sparse(g, s, p, need, b, e->stream);
+  b = SparseBufs{e->d_wlist, e->wlist_cap, e->st.stats + STAT_COUNT, e->d_chunk_cnt,
+                 e->d_chunk_off, e->d_touched};
+  return hipSuccess;
+}
+
+// Row-atomic push of the frontier of round p.round over g: lane-parallel when the rows allow it
+// (n_words = that frontier's nonzero words, which sizes the (peer, word) list), else per source.
+hipError_t launch_scatter_atomic(p2pg_engine* e, const DevGraph& g, const RoundParams& p,
+                                 uint64_t n_words) {
+  DevState& s = e->st;
+  if (!sparse_scatter_on(e))
+    return launch_gossip_scatter(g, s, p, e->d_hub, e->n_hub, false, e->stream);
+  SparseBufs b;
+  hipError_t r = sparse_bufs(e, (int64_t)n_words, b);
+  if (r != hipSuccess) return r;
+  return launch_gossip_scatter_sparse(g, s, p, (int64_t)n_words, b, e->stream);
+}
+
+// Can the fused rounds' hub pushes run by atomics (launch_wide_push_e)?
+bool wide_atomic_on(const p2pg_engine* e) {
+  return e->wide_atomic && e->W <= 64 && (e->W <= PACK_W_MAX_PLAIN || e->st.AW[0]);
 }
 
 // After the stream synced on a round whose push ran lane-parallel: the list must have held
@@ -437,6 +460,7 @@ int p2pg_create(const p2pg_config* cfg, p2pg_engine** out) {
   if (const char* t = std::getenv("P2PG_V_THRESH")) e->v_thresh = std::atof(t);
   if (const char* f = std::getenv("P2PG_FUSED")) e->fused = std::strcmp(f, "0") != 0;
   if (const char* f = std::getenv("P2PG_SPARSE_LP")) e->sparse_lp = std::strcmp(f, "0") != 0;
+  if (const char* f = std::getenv("P2PG_WIDE_ATOMIC")) e->wide_atomic = std::strcmp(f, "0") != 0;
   if (const char* m = std::getenv("P2PG_GOSSIP_PUSH"))
     e->push_mode = !std::strcmp(m, "atomic") ? 1 : (!std::strcmp(m, "store") ? 2 : 0);
   HIPCHK(e, hipSetDevice(cfg->device));
@@ -522,13 +546,21 @@ int upload_graph(p2pg_engine* e, int64_t V, const int64_t* rowptr, const int32_t
   if (nnz) HIPCHK(e, hipMemcpy(e->d_colidx, colidx, sizeof(int32_t) * nnz, hipMemcpyHostToDevice));
   // gossip: (source, neighbour-chunk) items for sources wider than one chunk
   std::vector<int64_t> hub, hub_big;
+  std::vector<int32_t> wide_big;
   for (int64_t v = 0; v < V; ++v) {
     const int64_t d = rowptr[v + 1] - rowptr[v];
-    if (d > GCHUNK)
+    if (d > GCHUNK) {
+      if (d > HUB_T) wide_big.push_back((int32_t)v);
       for (int64_t c = 0; c * GCHUNK < d; ++c) {
         hub.push_back((v << 32) | c);
         if (d > HUB_T) hub_big.push_back((v << 32) | c);
       }
+    }
+  }
+  e->n_wide_big = (int64_t)wide_big.size();
+  if (!wide_big.empty()) {
+    HIPCHK(e, hipMalloc((void**)&e->d_wide_big, sizeof(int32_t) * wide_big.size()));
+    HIPCHK(e, hipMemcpy(e->d_wide_big, wide_big.data(), sizeof(int32_t) * wide_big.size(), hipMemcpyHostToDevice));
   }
   e->n_hub = (int64_t)hub.size();
   e->n_hub_big = (int64_t)hub_big.size();
@@ -745,7 +777,12 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
       // round), without hop/parent records
       p.store_f = (e->skip_frontier && !s.hop) ? 0 : 1;
       if ((rc = timed(e, 7, [&] {
-             return launch_gossip_fused(g, s, p, e->hp, e->d_hub_big, e->n_hub_big, e->stream);
+             const bool wa = wide_atomic_on(e);
+             hipError_t r = launch_gossip_fused(g, s, p, e->hp, e->d_hub_big, e->n_hub_big, wa,
+                                                e->stream);
+             if (r != hipSuccess || !wa) return r;
+             return launch_wide_push_e(g, s, p, e->d_hub_big, e->n_hub_big, e->d_wide_big,
+                                       e->n_wide_big, e->stream);
            })))
         return rc;
     } else {

@@ -1953,7 +1953,7 @@ bool gossip_fused_supported(const DevState& st) {
 
 hipError_t launch_gossip_fused(const DevGraph& g, const DevState& st, const RoundParams& p,
                                const HubPlan& hp, const int64_t* big_items, int64_t n_big,
-                               hipStream_t s) {
+                               bool skip_big, hipStream_t s) {
   if (!gossip_fused_supported(st)) return hipErrorInvalidValue;
   if (hp.n_items)
     hipLaunchKernelGGL((k_pull_hub_partial<false, true>), dim3(grid_tasks(hp.n_items)),
@@ -1979,7 +1979,7 @@ hipError_t launch_gossip_fused(const DevGraph& g, const DevState& st, const Roun
   if (hp.n_hubs)
     hipLaunchKernelGGL((k_pull_hub_finalize<true>), dim3(grid_tasks(hp.n_hubs)), dim3(256), 0,
                        s, g, st, p, hp);
-  if (n_big) {
+  if (n_big && !skip_big) {
     const int64_t nwords = (g.V + 31) >> 5;
     scatter_dispatch<true>(grid_tasks((n_big + 63) >> 6), g, st, p, big_items, n_big, nwords, s);
   }

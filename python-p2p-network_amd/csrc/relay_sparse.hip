@@ -308,6 +308,123 @@ __global__ __launch_bounds__(256) void k_touched_bits(int64_t V, uint32_t* __res
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Dense (E-form) push of the pull hubs (deg > HUB_T) in fused rounds.  The per-source scatter
+// covers a wide source with one wave per 16-connection chunk, and every chunk wave recomputes
+// ALL the source's picks (only those landing in its chunk are kept): ceil(deg / 16) x the
+// Philox work, 625 x for a 10K-connection hub (c4: ~0.8 ms per early fused round for 764
+// hubs).  Here the picks run once:
+//   k_wide_zero: the receiver-slot E rows of every active hub are zeroed (its nf packed words,
+//                or W words unpacked) -- receivers gather them whole;
+//   k_wide_push: one wave per hub, lane = (word, bit): Philox + Floyd picks, then per pick one
+//                atomicOr of the message bit into E[r&1][rev[slot]] at the word's packed
+//                position; a pick that finds the word still zero counts one nonzero (sender,
+//                target, word) mask.  Churn-dropped connections keep zero rows.
+// Atomics suit hubs: they carry few bits per round (a hub receives each message once).  The
+// same path for the first dense round's deg > GCHUNK sources (625K of them in c4) measured
+// slower than their chunk items (zeroing 2.4 ms + picks 1.0 ms vs ~1.7 ms), and a (source,
+// word) list with merged masks was 3x slower for hubs (many bits per word: long merge loops).
+static_assert(GCHUNK >= 16, "wide sources must have deg > fanout (<= 16)");
+
+// Metadata lane = (item 4i + lane / 16, slot lane % 16): 4 chunk items per wave pass, all their
+// row offsets / word masks / receiver slots gathered at once; then one store instruction per
+// receiver row, lane = word (coalesced: a lane-per-row store pattern scattered 8 B writes over
+// 64 rows per instruction and took 16 ms in c4's first dense round)
+__global__ __launch_bounds__(256) void k_wide_zero(DevGraph g, DevState st, RoundParams p,
+                                                   const int64_t* __restrict__ items,
+                                                   int64_t n_items) {
+  const int lane = threadIdx.x & 63;
+  const int W = st.W;
+  const int cur = p.round & 1;
+  uint64_t* __restrict__ Eo = st.E[cur];
+  const uint64_t* __restrict__ AWc = st.AW[cur];
+  for (int64_t i0 = ((int64_t)blockIdx.x * WPB + wave_in_block()) * 4; i0 < n_items;
+       i0 += (int64_t)gridDim.x * WPB * 4) {
+    const int64_t it = i0 + (lane >> 4);
+    const int s = lane & 15;
+    int nf = 0;
+    uint32_t row = 0;
+    if (it < n_items) {
+      const int64_t item = items[it];
+      const int64_t v = item >> 32;
+      if (bit_test(st.A[cur], v)) {
+        const int64_t rb = g.rowptr[v], deg = g.rowptr[v + 1] - rb;
+        const int64_t nb = (item & 0xFFFFFFFFll) * GCHUNK;
+        if (nb + s < deg) {
+          row = g.rev[rb + nb + s];
+          nf = AWc ? __popcll(AWc[v]) : W;
+        }
+      }
+    }
+    for (uint64_t m = __ballot(nf > 0); m; m &= m - 1ull) {
+      const int l = __builtin_ctzll(m);
+      const uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)row, l);
+      const int n = __builtin_amdgcn_readlane(nf, l);
+      if (lane < n) st_row(&Eo[(int64_t)r * W + lane], 0ull);
+    }
+  }
+}
+
+template <bool CHURN, int K>
+__global__ __launch_bounds__(256) void k_wide_push(DevGraph g, DevState st, RoundParams p,
+                                                   const int32_t* __restrict__ wide,
+                                                   int64_t n_wide) {
+  __shared__ uint32_t own_all[WPB][64];
+  const int lane = threadIdx.x & 63;
+  const int wib = wave_in_block();
+  uint32_t* own = own_all[wib];
+  const int W = st.W;
+  const int cur = p.round & 1;
+  uint64_t* __restrict__ Eo = st.E[cur];
+  const uint64_t* __restrict__ AWc = st.AW[cur];
+  const uint32_t k = K > 0 ? (uint32_t)K : (uint32_t)p.fanout;
+  uint64_t pushed = 0;
+  for (int64_t i = (int64_t)blockIdx.x * WPB + wib; i < n_wide; i += (int64_t)gridDim.x * WPB) {
+    const int64_t v = ldc(wide + i);
+    if (!((ldc(st.A[cur] + (v >> 5)) >> (v & 31)) & 1u)) continue;
+    const int64_t rb = ldc(g.rowptr + v);
+    const uint32_t deg = (uint32_t)(ldc(g.rowptr + v + 1) - rb);
+    const uint64_t am = AWc ? ldc(AWc + v) : (W >= 64 ? ~0ull : (1ull << W) - 1ull);
+    const uint32_t gv = gidx_s(g, v);
+    // lane = word of the row
+    const uint64_t f = lane < W && ((am >> lane) & 1ull) ? st.F[cur][v * W + lane] : 0ull;
+    const uint32_t pos_w = AWc ? (uint32_t)__popcll(am & ((1ull << lane) - 1ull)) : (uint32_t)lane;
+    const uint32_t bc = (uint32_t)__popcll(f);
+    const uint32_t binc = wave_scan_u32(bc);
+    const uint32_t bpos = binc - bc;
+    const uint32_t btot = (uint32_t)__builtin_amdgcn_readlane((int)binc, 63);
+    for (uint32_t b0 = 0; b0 < btot; b0 += 64) {
+      // lane = bit b0 + lane of the row (owner lane = its word)
+      const int ow = pass_owner(own, lane, bpos, bc, b0);
+      const uint32_t gpos = bperm(ow, bpos), epos = bperm(ow, pos_w);
+      const uint64_t gf = bperm64(ow, f);
+      if (b0 + (uint32_t)lane < btot) {
+        const uint32_t b = select_bit64(gf, b0 + (uint32_t)lane - gpos);
+        const uint32_t mg = p.msg_base + (uint32_t)ow * 64u + b;
+        uint32_t pk[K > 0 ? K : 16];
+        if constexpr (K > 0)
+          gossip_picks_t<K>((uint32_t)p.round, gv, mg, deg, p.gseed_lo, p.gseed_hi, pk);
+        else
+          gossip_picks((uint32_t)p.round, gv, mg, deg, (int)k, p.gseed_lo, p.gseed_hi, pk);
+        uint64_t old[K > 0 ? K : 16];  // (K > 0: constant trip counts, unrolled)
+        for (uint32_t q = 0; q < (K > 0 ? (uint32_t)K : k); ++q) {
+          old[q] = 1ull;  // (not counted)
+          const int64_t slot = rb + (int64_t)pk[q];
+          if (CHURN && churn_dropped((uint32_t)p.round, gv, gidx(g, g.colidx[slot]), p.churn_thr,
+                                     p.cseed_lo, p.cseed_hi))
+            continue;  // a lost send: the connection's row stays zero
+          old[q] = atomicOr((unsigned long long*)&Eo[(int64_t)g.rev[slot] * W + epos], 1ull << b);
+        }
+        // the returned words are used only after all picks are issued (one wait, not k)
+        for (uint32_t q = 0; q < (K > 0 ? (uint32_t)K : k); ++q) pushed += old[q] == 0ull ? 1u : 0u;
+      }
+    }
+  }
+  uint64_t c[STAT_N] = {0, 0, 0, 0, 0, 0, 0, 0};
+  c[ST_SCATTER] = pushed;
+  flush_stats(st.stats, c, lane);
+}
+
 }  // namespace
 
 bool gossip_scatter_sparse_supported(const DevState& st) {
@@ -340,6 +457,28 @@ hipError_t launch_gossip_scatter_sparse(const DevGraph& g, const DevState& st,
   const int64_t ntasks = (g.V + 31) >> 5;
   hipLaunchKernelGGL(k_touched_bits, dim3((unsigned)std::min<int64_t>((ntasks + 255) / 256, 4096)),
                      dim3(256), 0, s, g.V, st.T[(p.round & 1) ^ 1], b.touched);
+  return hipGetLastError();
+}
+
+hipError_t launch_wide_push_e(const DevGraph& g, const DevState& st, const RoundParams& p,
+                              const int64_t* items, int64_t n_items, const int32_t* wide,
+                              int64_t n_wide, hipStream_t s) {
+  if (st.W > 64 || (st.W > PACK_W_MAX_PLAIN && !st.AW[p.round & 1])) return hipErrorInvalidValue;
+  if (n_items <= 0 || n_wide <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_wide_zero, dim3(grid_tasks((n_items + 3) >> 2)), dim3(256), 0, s, g, st,
+                     p, items, n_items);
+  const int grid = grid_tasks(n_wide);
+  const bool ch = p.churn_thr != 0;
+#define P2PG_WIDE(CH, KK) \
+  hipLaunchKernelGGL((k_wide_push<CH, KK>), dim3(grid), dim3(256), 0, s, g, st, p, wide, n_wide)
+  switch (p.fanout) {
+    case 1: if (ch) P2PG_WIDE(true, 1); else P2PG_WIDE(false, 1); break;
+    case 2: if (ch) P2PG_WIDE(true, 2); else P2PG_WIDE(false, 2); break;
+    case 3: if (ch) P2PG_WIDE(true, 3); else P2PG_WIDE(false, 3); break;
+    case 4: if (ch) P2PG_WIDE(true, 4); else P2PG_WIDE(false, 4); break;
+    default: if (ch) P2PG_WIDE(true, 0); else P2PG_WIDE(false, 0); break;
+  }
+#undef P2PG_WIDE
   return hipGetLastError();
 }
 

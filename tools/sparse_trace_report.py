@@ -5,7 +5,8 @@ import glob
 import sys
 
 KEYS = ("k_sparse_words<false>", "k_chunk_scan", "k_sparse_words<true>", "k_sparse_push",
-        "k_touched_bits", "k_gossip_update1", "k_pull1", "k_gossip_scatter")
+        "k_touched_bits", "k_gossip_update1", "k_pull1", "k_gossip_scatter", "k_wide_zero",
+        "k_wide_push", "k_gossip_fused")
 f = glob.glob(sys.argv[1] + "/**/*kernel_trace.csv", recursive=True)[0]
 rows = sorted(csv.DictReader(open(f)), key=lambda r: int(r["Start_Timestamp"]))
 per = {k: [] for k in KEYS}
