@@ -49,8 +49,10 @@ def calib(d):
 def cls(name):
     """rocprof kernel name -> bench.py timer class (include/p2pgpu.h P2PG_KCLASS_N)."""
     tmpl = name.split("<", 1)[1].split(">(")[0] if "<" in name else ""
-    if "k_gossip_fused" in name:
-        return "gossip_fused"
+    if "k_gossip_fused" in name or "k_wide_zero" in name or "k_wide_push" in name:
+        return "gossip_fused"  # (the hub pushes ride in the fused rounds' timed launch group)
+    if any(x in name for x in ("k_sparse_words", "k_chunk_scan", "k_sparse_push", "k_touched_bits")):
+        return "gossip_scatter_atomic"
     if "k_gossip_scatter" in name:
         return "gossip_scatter_store" if tmpl.rstrip().endswith("true") else "gossip_scatter_atomic"
     if "k_pull" in name:
@@ -77,8 +79,11 @@ def main():
         a = agg[k]
         a["fetch"] += c.get("FETCH_SIZE", 0.0) * 1024 * rf
         a["write"] += c.get("WRITE_SIZE", 0.0) * 1024 * wf
-        # hub partial/finalize kernels ride in the same timed launch group as their k_pull1
-        a["n"] += 1 if ("FETCH_SIZE" in c and "k_pull_hub" not in name) else 0
+        # helper kernels (hub pull partial/finalize, hub pushes, sparse-push list builders) ride
+        # in the same timed launch group as their main kernel: count launches of the main one
+        helper = any(x in name for x in ("k_pull_hub", "k_wide_", "k_sparse_words", "k_chunk_scan",
+                                         "k_touched_bits"))
+        a["n"] += 1 if ("FETCH_SIZE" in c and not helper) else 0
         a["ns"] += c["ns"] if "FETCH_SIZE" in c else 0
     res = {"workload": wl, "calibration": cal, "source": run_dir, "kernels": {}}
     # the scatter and both consume kernels share class names with bench.py's timers
