@@ -297,6 +297,10 @@ def test_gpu_gossip_push_forms_match_golden(name, push, monkeypatch):
     ("ws", dict(V=500, k=6, b=0.2), 200, 300_000_000, 2),
     ("ba", dict(V=150, m=20), 4160, 0, 3),
     ("gnp", dict(V=300, k=5.0), 130, 0, 7),
+    # packed rows (AW planes, 8 < W <= 64): the lane-parallel sparse push with whole 64-bit
+    # words of bits per hub (long merge groups), fused rounds' hub pushes by atomics, churn
+    ("hub", dict(V=1500, m=3, star=1100), 4096, 0, 3),
+    ("hub", dict(V=1500, m=3, star=700), 1024, 300_000_000, 5),
 ])
 def test_gpu_gossip_push_forms_match_oracle(kind, p, M, thr, fanout, push, monkeypatch):
     """Row atomics, edge stores with fused pull+scatter rounds (k_gossip_fused: every round
