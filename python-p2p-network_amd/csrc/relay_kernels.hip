@@ -731,6 +731,83 @@ __global__ __launch_bounds__(256) void k_gossip_update1(DevGraph g, DevState st,
   flush_stats(st.stats, c, lane);
 }
 
+// The same update for narrow rows (W <= 32: one rank's share of a message split): G = 64 / WP
+// touched peers per wave pass, lane = (peer g, word w), WP = W rounded up to a power of two, so
+// the per-peer fixed work (ballots, counters, stores) is shared by G peers.  The touched peers
+// of a task word are picked by select-nth-bit; the next task's word is a scalar load issued one
+// task ahead.  Same results as k_gossip_update.
+template <int LW>
+__global__ __launch_bounds__(256) void k_gossip_update_g(DevGraph g, DevState st, RoundParams p) {
+  constexpr int WP = 1 << LW, G = 64 >> LW;
+  const int lane = threadIdx.x & 63;
+  const int wib = wave_in_block();
+  const int W = st.W;
+  const int cur = p.round & 1;
+  uint64_t* __restrict__ nx = st.next[cur];
+  uint64_t* __restrict__ Fc = st.F[cur];
+  uint32_t* __restrict__ Tc = st.T[cur];
+  uint64_t* __restrict__ AWc = st.AW[cur];
+  const int64_t ntasks = (g.V + 31) >> 5;
+  const int grp = lane >> LW, w = lane & (WP - 1);
+  const uint64_t segm = WP >= 64 ? ~0ull : (1ull << WP) - 1ull;
+  uint64_t c[STAT_N] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int64_t tstride = (int64_t)gridDim.x * WPB;
+  int64_t task = (int64_t)blockIdx.x * WPB + wib;
+  uint32_t tw_next = task < ntasks ? ldc(&Tc[task]) : 0u;
+  for (; task < ntasks; task += tstride) {
+    const uint32_t tw0 = tw_next;
+    tw_next = task + tstride < ntasks ? ldc(&Tc[task + tstride]) : 0u;
+    const uint32_t tw = tw0 & phase_mask(p, task);
+    if (!tw) {
+      if (lane == 0 && p.phase != 1) st.A[cur][task] = 0u;  // put_active(.., 0, ..)
+      continue;
+    }
+    if (lane == 0) Tc[task] = tw0 & ~tw;  // consumed (the other phase's bits stay)
+    const uint32_t n = (uint32_t)__popc(tw);
+    uint32_t aw = 0;
+    for (uint32_t pb = 0; pb < n; pb += G) {
+      const uint32_t idx = pb + (uint32_t)grp;
+      const bool peer = idx < n;
+      const bool ok = peer && w < W;
+      const int64_t u = (task << 5) + (peer ? select_bit32(tw, idx) : 0u);
+      uint64_t x = 0, s = 0;
+      if (ok) x = nx[u * W + w];
+      if (x) {
+        s = st.seen[u * W + w];
+        st_prow(&nx[u * W + w], 0ull);
+        c[ST_AUX] += 1;  // touched (pushed-to) words consumed
+      }
+      const uint64_t nw = x & ~s;
+      const uint64_t wm = (__ballot(nw != 0ull) >> (grp * WP)) & segm;  // this peer's new words
+      if (nw) st_prow(&st.seen[u * W + w], s | nw);
+      if (ok && wm) st_prow(&Fc[u * W + w], nw);
+      if (wm) {
+        const int64_t deg = g.rowptr[u + 1] - g.rowptr[u];
+        // relays per first receipt: gossip min(k, deg); flood (rows materialized by a topology
+        // update) deg - 1, the sender's connection being excluded (node.py:106-112)
+        const uint64_t fan = p.mode == 0 ? (uint64_t)(deg > 0 ? deg - 1 : 0)
+                                         : (uint64_t)(deg < p.fanout ? deg : p.fanout);
+        if (nw) {
+          const uint64_t pc = (uint64_t)__popcll(nw);
+          c[ST_NEW] += pc;
+          c[ST_RELAYS] += pc * fan;
+          c[ST_ACTIVE_W] += 1;
+          c[ST_WEDGES] += (uint64_t)deg;
+        }
+        if (w == 0) {
+          if (AWc) AWc[u] = wm;
+          c[ST_ACTIVE_V] += 1;
+          c[ST_DEG_ACT] += (uint64_t)deg;
+        }
+      }
+      // distinct bits per peer: the wave sum of (w == 0 lanes' bits) is their OR
+      aw |= wave_reduce_u32<false>(w == 0 && wm ? 1u << (u & 31) : 0u);
+    }
+    if (lane == 0) put_active(st.A[cur], task, aw, p);
+  }
+  flush_stats(st.stats, c, lane);
+}
+
 // Messages in flight after round r = p.round - 1, as row pushes into next[p.round&1] + T bits
 // (the form k_gossip_update consumes), one wave per receiver u, lane = word, serial over u's
 // slots (not a hot path):
@@ -1892,7 +1969,22 @@ hipError_t launch_gossip_update(const DevGraph& g, const DevState& st, const Rou
     const char* e = std::getenv("P2PG_UPDATE1");
     return !(e && std::strcmp(e, "0") == 0);
   }();
-  if (st.W <= 64 && pipelined)
+  static const bool narrow = [] {  // P2PG_UPDATE_G=0: one peer per wave at W <= 32 too (A/B)
+    const char* e = std::getenv("P2PG_UPDATE_G");
+    return !(e && std::strcmp(e, "0") == 0);
+  }();
+  if (narrow && st.W <= 32) {
+    int lw = 0;
+    while ((1 << lw) < st.W) ++lw;
+    switch (lw) {
+      case 0: hipLaunchKernelGGL(k_gossip_update_g<0>, dim3(grid), dim3(256), 0, s, g, st, p); break;
+      case 1: hipLaunchKernelGGL(k_gossip_update_g<1>, dim3(grid), dim3(256), 0, s, g, st, p); break;
+      case 2: hipLaunchKernelGGL(k_gossip_update_g<2>, dim3(grid), dim3(256), 0, s, g, st, p); break;
+      case 3: hipLaunchKernelGGL(k_gossip_update_g<3>, dim3(grid), dim3(256), 0, s, g, st, p); break;
+      case 4: hipLaunchKernelGGL(k_gossip_update_g<4>, dim3(grid), dim3(256), 0, s, g, st, p); break;
+      default: hipLaunchKernelGGL(k_gossip_update_g<5>, dim3(grid), dim3(256), 0, s, g, st, p); break;
+    }
+  } else if (st.W <= 64 && pipelined)
     hipLaunchKernelGGL(k_gossip_update1, dim3(grid), dim3(256), 0, s, g, st, p);
   else
     hipLaunchKernelGGL(k_gossip_update, dim3(grid), dim3(256), 0, s, g, st, p);
