@@ -835,7 +835,9 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
     // the lane-parallel sparse push sizes its (peer, word) list by the frontier's word count
     if (!use_e && !have_tot && sparse_scatter_on(e) && (rc = read_stats())) return rc;
     if ((rc = timed(e, use_e ? 6 : 2, [&] {
-           return use_e ? launch_gossip_scatter(g, s, p, e->d_hub, e->n_hub, true, e->stream)
+           return use_e ? launch_gossip_scatter(g, s, p, e->d_hub, e->n_hub, true, e->stream,
+                                                e->d_hub_big, e->n_hub_big, e->d_wide_big,
+                                                e->n_wide_big)
                         : launch_scatter_atomic(e, g, p, tot[ST_ACTIVE_W]);
          })))
       return rc;

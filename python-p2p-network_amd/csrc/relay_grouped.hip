@@ -73,7 +73,11 @@ struct GStage {
 #ifndef P2PG_GROUPED_WAVES
 #define P2PG_GROUPED_WAVES 4  // <= 128 VGPRs
 #endif
-template <bool CHURN, int K, int LW>
+// PO (push only): the first dense round after an update -- the batch peers are the round's
+// active peers, their arrivals are their own frontier rows F[r&1] (dedup, counters, bitmaps were
+// done by the update), and only the picks and the flush run (replaces one wave per source with
+// 8 of 64 lanes busy at W = 8).
+template <bool CHURN, int K, int LW, bool PO = false>
 __global__ __launch_bounds__(256, P2PG_GROUPED_WAVES) void k_gossip_fused_grouped(DevGraph g, DevState st, RoundParams p) {
   using Lds = GroupedLds<LW>;
   constexpr int WP = Lds::WP;
@@ -108,13 +112,13 @@ __global__ __launch_bounds__(256, P2PG_GROUPED_WAVES) void k_gossip_fused_groupe
   for (int64_t task = (int64_t)blockIdx.x * WPB + wave_in_block(); task < ntasks;
        task += (int64_t)gridDim.x * WPB) {
     const int64_t u0 = task << 5;
-    const uint32_t sat0 = st.S[task];
+    const uint32_t sat0 = PO ? 0u : st.S[task];
     const int nv = V - u0 < 32 ? (int)(V - u0) : 32;
-    uint32_t todo = ~sat0;
+    uint32_t todo = PO ? st.A[cur][task] : ~sat0;
     if (g.H) todo &= ~g.H[task];  // hubs: k_pull_hub_* and the chunk-item scatter
     if (nv < 32) todo &= (1u << nv) - 1u;
     if (!todo) {
-      if (lane == 0) st.A[cur][task] = 0u;
+      if (!PO && lane == 0) st.A[cur][task] = 0u;
       continue;
     }
     int64_t rp = 0;
@@ -144,7 +148,8 @@ __global__ __launch_bounds__(256, P2PG_GROUPED_WAVES) void k_gossip_fused_groupe
       q.rb0 = rb0;
       q.rb1 = readlane64(rp, b0 + n);
       const bool mine = gl < n && ((todo >> (b0 + gl)) & 1u);
-      if (mine && wvalid) q.s = ld_once(&st.seen[(u0 + b0 + gl) * W + wl]);
+      // PO: the peer's frontier row (its new receipts) instead of its seen row
+      if (mine && wvalid) q.s = ld_once(&(PO ? Fc : st.seen)[(u0 + b0 + gl) * W + wl]);
       int gj = 0;  // batch peer owning slot rb0 + lane
       for (int i = 1; i < n; ++i) gj += readlane64(rp, b0 + i) - rb0 <= (int64_t)lane;
       q.rcv = rb0 + lane < q.rb1 && ((todo >> (b0 + gj)) & 1u);
@@ -156,7 +161,7 @@ __global__ __launch_bounds__(256, P2PG_GROUPED_WAVES) void k_gossip_fused_groupe
     auto activity = [&](GStage& q) {
       q.aword = 0;
       q.amv = 0;
-      if (q.rcv) {
+      if (!PO && q.rcv) {
         q.aword = Ap[q.v >> 5];
         if (packed) q.amv = AWp[q.v];
       }
@@ -164,7 +169,7 @@ __global__ __launch_bounds__(256, P2PG_GROUPED_WAVES) void k_gossip_fused_groupe
     // lane (g, w): need = words of peer g still open; the owner's slot range within 64 lanes
     auto need_of = [&](const GStage& q) -> uint64_t {
       const bool mine = gl < q.n && ((todo >> (q.b0 + gl)) & 1u);
-      return mine ? fm & ~q.s : 0ull;
+      return mine ? (PO ? ~0ull : fm & ~q.s) : 0ull;
     };
     auto my_slots = [&](const GStage& q, int64_t cb) -> uint64_t {
       const int bi = gl < q.n ? q.b0 + gl : q.b0;
@@ -201,7 +206,7 @@ __global__ __launch_bounds__(256, P2PG_GROUPED_WAVES) void k_gossip_fused_groupe
     auto first_gathers = [&](GStage& q) {
       q.mr = 0;
       X[0] = X[1] = X[2] = X[3] = 0ull;
-      if (q.n == 0) return;
+      if (PO || q.n == 0) return;
       const uint64_t need = need_of(q);
       const uint64_t am = active_slots(q, q.rb0, q.v, q.rcv, q.aword);
       const uint64_t ms = my_slots(q, q.rb0);  // ds_bpermute: evaluated by every lane
@@ -244,7 +249,8 @@ __global__ __launch_bounds__(256, P2PG_GROUPED_WAVES) void k_gossip_fused_groupe
       // 1. arrivals: the first gathers (in flight since the last step) + the rest
       uint64_t acc = (X[0] | X[1]) | (X[2] | X[3]);
       const uint64_t need = need_of(a);
-      {
+      if (PO) acc = a.s;  // the frontier row
+      if (!PO) {
         uint64_t mg = a.mr;
         while (__ballot(mg != 0ull)) {
           gathers(a.rb0, mg, a.amv);
@@ -289,25 +295,27 @@ __global__ __launch_bounds__(256, P2PG_GROUPED_WAVES) void k_gossip_fused_groupe
       const uint64_t nw = acc & need;
       const uint64_t wm_all = __ballot(nw != 0ull);
       const uint32_t grp = (uint32_t)((wm_all >> (gl * WP)) & gmask);  // my peer's active words
-      if (nw) st_frow(&st.seen[u * W + wl], a.s | nw);
-      if (mine && grp && wvalid && p.store_f) st_frow(&Fc[u * W + wl], nw);
-      if (nw) {
-        const uint32_t pc = (uint32_t)__popcll(nw);
-        c[ST_NEW] += pc;
-        c[ST_RELAYS] += pc * (degg < (uint32_t)k ? degg : (uint32_t)k);
-        c[ST_ACTIVE_W] += 1;
-        c[ST_WEDGES] += degg;
-      }
-      if (mine && wl == 0 && grp) {
-        if (packed) st.AW[cur][u] = grp;
-        c[ST_ACTIVE_V] += 1;
-        c[ST_DEG_ACT] += degg;
+      if (!PO) {
+        if (nw) st_frow(&st.seen[u * W + wl], a.s | nw);
+        if (mine && grp && wvalid && p.store_f) st_frow(&Fc[u * W + wl], nw);
+        if (nw) {
+          const uint32_t pc = (uint32_t)__popcll(nw);
+          c[ST_NEW] += pc;
+          c[ST_RELAYS] += pc * (degg < (uint32_t)k ? degg : (uint32_t)k);
+          c[ST_ACTIVE_W] += 1;
+          c[ST_WEDGES] += degg;
+        }
+        if (mine && wl == 0 && grp) {
+          if (packed) st.AW[cur][u] = grp;
+          c[ST_ACTIVE_V] += 1;
+          c[ST_DEG_ACT] += degg;
+        }
+        aw |= (uint32_t)__ballot(lane < n && ((wm_all >> (lane * WP)) & gmask) != 0u) << a.b0;
+        const uint64_t open = __ballot(mine && wvalid && (a.s | nw) != fm);
+        const bool done_i = lane < n && ((todo >> (a.b0 + lane)) & 1u) && ((open >> (lane * WP)) & gmask) == 0ull;
+        sat |= (uint32_t)__ballot(done_i) << a.b0;
       }
       const uint32_t gi = lane < n ? (uint32_t)((wm_all >> (lane * WP)) & gmask) : 0u;
-      aw |= (uint32_t)__ballot(gi != 0u) << a.b0;
-      const uint64_t open = __ballot(mine && wvalid && (a.s | nw) != fm);
-      const bool done_i = lane < n && ((todo >> (a.b0 + lane)) & 1u) && ((open >> (lane * WP)) & gmask) == 0ull;
-      sat |= (uint32_t)__ballot(done_i) << a.b0;
       if (!wm_all) return;
       // 4. this round's pushes: picks into the (slot, word) table, then the flush
       if (lane < n) L.wmask[lane] = gi;
@@ -407,7 +415,7 @@ __global__ __launch_bounds__(256, P2PG_GROUPED_WAVES) void k_gossip_fused_groupe
       if (sA.n == 0) { last(sD); break; }
     }
     wave_lds_sync();
-    if (lane == 0) {
+    if (!PO && lane == 0) {
       st.A[cur][task] = aw;
       if (sat != sat0) st.S[task] = sat;
     }
@@ -422,12 +430,12 @@ __global__ __launch_bounds__(256, P2PG_GROUPED_WAVES) void k_gossip_fused_groupe
   }
 }
 
-template <bool CH, int KT>
+template <bool CH, int KT, bool PO = false>
 hipError_t launch_lw(int lw, const DevGraph& g, const DevState& st, const RoundParams& p, hipStream_t s) {
   const int64_t ntasks = (g.V + 31) >> 5;
 #define P2PG_GROUPED(LWV)                                                                    \
-  hipLaunchKernelGGL((k_gossip_fused_grouped<CH, KT, LWV>),                                \
-                     dim3(balanced_grid(k_gossip_fused_grouped<CH, KT, LWV>, ntasks)), dim3(256), \
+  hipLaunchKernelGGL((k_gossip_fused_grouped<CH, KT, LWV, PO>),                            \
+                     dim3(balanced_grid(k_gossip_fused_grouped<CH, KT, LWV, PO>, ntasks)), dim3(256), \
                      0, s, g, st, p)
   switch (lw) {
     case 0: P2PG_GROUPED(0); break;
@@ -451,6 +459,17 @@ hipError_t launch_gossip_fused_grouped(const DevGraph& g, const DevState& st, co
   const bool ch = p.churn_thr != 0;
   if (p.fanout == 3) return ch ? launch_lw<true, 3>(lw, g, st, p, s) : launch_lw<false, 3>(lw, g, st, p, s);
   return ch ? launch_lw<true, 0>(lw, g, st, p, s) : launch_lw<false, 0>(lw, g, st, p, s);
+}
+
+hipError_t launch_gossip_push_grouped(const DevGraph& g, const DevState& st, const RoundParams& p,
+                                      hipStream_t s) {
+  if (st.W > GROUPED_W_MAX || st.W < 1) return hipErrorInvalidValue;
+  int lw = 0;
+  while ((1 << lw) < st.W) ++lw;
+  const bool ch = p.churn_thr != 0;
+  if (p.fanout == 3)
+    return ch ? launch_lw<true, 3, true>(lw, g, st, p, s) : launch_lw<false, 3, true>(lw, g, st, p, s);
+  return ch ? launch_lw<true, 0, true>(lw, g, st, p, s) : launch_lw<false, 0, true>(lw, g, st, p, s);
 }
 
 }  // namespace p2pg

@@ -2009,9 +2009,12 @@ void scatter_dispatch(int grid, const DevGraph& g, const DevState& st, const Rou
 #undef P2PG_SCATTER
 }
 
+static bool grouped_enabled();
+
 hipError_t launch_gossip_scatter(const DevGraph& g, const DevState& st, const RoundParams& p,
                                  const int64_t* hub_items, int64_t n_hub_items, bool store_e,
-                                 hipStream_t s) {
+                                 hipStream_t s, const int64_t* big_items, int64_t n_big,
+                                 const int32_t* wide_big, int64_t n_wide_big) {
   // blocks cap: P2PG_SCATTER_GRID (default GRID_MAX)
   static const int64_t cap = [] {
     const char* e = std::getenv("P2PG_SCATTER_GRID");
@@ -2020,6 +2023,16 @@ hipError_t launch_gossip_scatter(const DevGraph& g, const DevState& st, const Ro
   }();
   const int grid = (int)std::min<int64_t>(
       grid_tasks_uncapped(((g.V + 31) >> 5) + ((n_hub_items + 63) >> 6)), cap);
+  static const bool push_grouped = [] {  // P2PG_PUSH_GROUPED=0: one wave per source (A/B)
+    const char* e = std::getenv("P2PG_PUSH_GROUPED");
+    return !(e && std::strcmp(e, "0") == 0);
+  }();
+  if (store_e && push_grouped && grouped_enabled() && st.W <= GROUPED_W_MAX &&
+      (n_big == 0 || (big_items && wide_big))) {
+    hipError_t r = launch_gossip_push_grouped(g, st, p, s);
+    if (r != hipSuccess) return r;
+    return launch_wide_push_e(g, st, p, big_items, n_big, wide_big, n_wide_big, s);
+  }
   if (store_e)
     scatter_dispatch<true>(grid, g, st, p, hub_items, n_hub_items, 0, s);
   else
