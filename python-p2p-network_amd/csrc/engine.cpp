@@ -68,8 +68,11 @@ struct p2pg_engine {
   unsigned long long* h_seg_cnt = nullptr;  // pinned
   bool begun = false;                 // p2pg_step_begin ran this round's phase 0
   bool last_push_e = false;    // gossip: pushes of the previous round went to E (dense)
-  double e_thresh = 0.04;      // store-mode when active words >= thresh * active rows * W
-                               // (c4 A/B, interleaved runs: 0.04 320.4 ms vs 0.1 324.3 ms)
+  double e_thresh = -1.0;      // store-mode when active words >= thresh * active rows * W;
+                               // default (< 0) by row width, see alloc_state
+                               // (c4 A/B, interleaved runs: 0.04 320.4 ms vs 0.1 324.3 ms, round 1;
+                               // with the lane-parallel sparse push (round 2) W = 64: 0.04 / 0.06 /
+                               // 0.08 -> 278.4 / 275.5 / 275.2 ms, W = 8: 89.1 / 89.4 / 89.5 ms)
   double v_thresh = 0.3;       // ... and active rows >= v_thresh * V: a dense round visits every
                                // unsaturated peer, a sparse one only the pushed-to rows (narrow
                                // rows: word density alone is high whenever anything is active)
@@ -388,6 +391,7 @@ int alloc_state(p2pg_engine* e) {
   free_state(e);
   DevState& s = e->st;
   s.W = e->W;
+  if (e->e_thresh < 0.0) e->e_thresh = e->W > GROUPED_W_MAX ? 0.06 : 0.04;
   s.M = e->M;
   e->plane_bytes = (size_t)e->V * e->W * sizeof(uint64_t);
   e->bm_bytes = (size_t)((e->V + 31) / 32) * sizeof(uint32_t);
