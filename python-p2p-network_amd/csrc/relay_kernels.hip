@@ -1964,7 +1964,14 @@ hipError_t launch_materialize(const DevGraph& g, const DevState& st, const Round
 
 hipError_t launch_gossip_update(const DevGraph& g, const DevState& st, const RoundParams& p,
                                 hipStream_t s) {
-  const int grid = grid_tasks((g.V + 31) >> 5);
+  // blocks cap (P2PG_UPDATE_GRID): c4 A/B, interleaved, update ms per step: 256 / 512 / 1024 /
+  // 2048 (GRID_MAX) / 4096 / 8192 blocks -> 40.8 / 25.7 / 18.25 / 18.7 / 20.0 / 22.9
+  static const int64_t cap = [] {
+    const char* e = std::getenv("P2PG_UPDATE_GRID");
+    const int64_t v = e ? std::atoll(e) : 1024;
+    return v > 0 ? v : (int64_t)1024;
+  }();
+  const int grid = (int)std::min<int64_t>(grid_tasks((g.V + 31) >> 5), cap);
   static const bool pipelined = [] {  // P2PG_UPDATE1=0: the unpipelined kernel (A/B only)
     const char* e = std::getenv("P2PG_UPDATE1");
     return !(e && std::strcmp(e, "0") == 0);
