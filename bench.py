@@ -223,6 +223,23 @@ def load_traffic(workload, kernel):
     return d.get("kernels", {}).get(kernel, {}).get("bytes_per_launch")
 
 
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` started without a launcher (WORLD_SIZE unset, N > 1): run the N ranks
+    as children of this process under torch.distributed.run (127.0.0.1 rendezvous) and return
+    their exit code.  Nothing here touches torch or the GPU -- the children initialise it, one
+    process per GPU (LOCAL_RANK = device) -- and this process only waits (no exec)."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this host driver
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -239,15 +256,27 @@ def main():
                     help="gloo stages the exchange through host memory (rehearsal with several "
                          "ranks on one GPU); nccl = RCCL over xGMI")
     args = ap.parse_args()
+    if args.gpus < 1:
+        raise SystemExit(f"--gpus {args.gpus}: need at least one rank")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        # a mislaunched job must not report an N = 1 (or partial) number as an N-GPU one
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}; launch with "
+                         f"--nproc-per-node {args.gpus} or without a launcher")
     dist = None
     if world > 1:
         import torch
         import torch.distributed as dist
-        local = local % max(torch.cuda.device_count(), 1)  # gloo rehearsal: ranks may share a GPU
+        ndev = torch.cuda.device_count()  # counts devices without initialising them
+        if args.dist_backend == "nccl" and world > ndev:
+            raise SystemExit(f"--gpus {world} with RCCL needs {world} GPUs, {ndev} visible "
+                             f"(--dist-backend gloo rehearses several ranks on one GPU)")
+        local = local % max(ndev, 1)  # gloo rehearsal: ranks may share a GPU
         torch.cuda.set_device(local)
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -278,9 +307,11 @@ def main():
         net = PartitionedNetwork(g, world, rank, TorchTransport(device=torch.device("cuda", local)), **common)
     else:
         # message axis, fixed total work: rank r runs broadcasts [lo, hi) of the M (global ids,
-        # so origins and Philox streams are the 1-GPU run's) on its own graph copy
-        if M % (64 * world):
-            raise SystemExit(f"--gpus {world}: {M} broadcasts do not split into whole 64-bit words")
+        # so origins and Philox streams are the 1-GPU run's) on its own graph copy.  4096 split
+        # into whole 64-bit words for N | 64; any other split is still exact (a rank's bit
+        # positions are local, its message ids global), only the rows are ragged
+        if M < world:
+            raise SystemExit(f"--gpus {world}: only {M} broadcasts to split")
         lo, hi = rank * M // world, (rank + 1) * M // world
         src = make_sources(g.V, M, seed=1)[lo:hi]
         net = GraphNetwork(g, msg_id_base=lo, **common)
@@ -378,6 +409,7 @@ def main():
         "survey_model_bytes_per_step": sb_step,
         "whole_step_frac_survey_model": sb_step / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBPS,
         "kernel_time_frac_of_step": kernel_ms_total / (elapsed / args.steps * 1e3),
+        "relays_per_step": relays // args.steps,
         "relays_per_step_per_gpu": relays / args.steps / world,
         "exchange_ms_per_step": (net.exchange_s * 1e3) if partitioned else 0.0,
         # compacted exchange: fraction of the boundary rows that had a non-zero word and travelled

@@ -132,8 +132,9 @@ int p2pg_run(p2pg_engine* e, int32_t max_rounds, p2pg_round_stats* per_round,
              int32_t* n_rounds);
 /* The first receipts of the most recent round, sorted by (peer, msg); parent = -1 at the
  * source.  Writes min(cap, count) records; *n_out = count (may exceed cap).
- * P2PG_ERR_STATE if that round's (or, for the parents, the previous round's) frontier was
- * not kept -- not reachable through p2pg_step / p2pg_run as specified above.               */
+ * A round without first receipts has none (*n_out = 0).  P2PG_ERR_STATE if that round's
+ * (or, for the parents, the previous round's) frontier was not kept -- not reachable through
+ * p2pg_step / p2pg_run as specified above.                                                 */
 int p2pg_get_new_deliveries(p2pg_engine* e, int64_t cap, int32_t* peer, int32_t* msg,
                             int32_t* hop, int32_t* parent, int64_t* n_out);
 /* Validation copies: seen [V][W] uint64 (W = ceil(M/64)); hop/parent [V][M] int32 need
@@ -180,7 +181,9 @@ int p2pg_exchange_unpack_live(p2pg_engine* e, int32_t plane, const void* dev_buf
 /* A round in two calls, so a vertex-partitioned rank overlaps the exchange of the last round's
  * rows with work: step_begin launches the pull / update of the peers with no ghost neighbour
  * (they need none of the exchanged rows) and returns at once; step_end runs the rest of the
- * round once the rows are unpacked (= p2pg_step).  p2pg_step alone does both.              */
+ * round once the rows are unpacked (= p2pg_step).  p2pg_step alone does both.  Between the
+ * two, snapshot / restore / update_edges / set_exchange / exchange packing are refused
+ * (P2PG_ERR_STATE): the round is half done.                                                */
 int p2pg_step_begin(p2pg_engine* e);
 int p2pg_step_end(p2pg_engine* e, p2pg_round_stats* out);
 /* ---- dynamic topology --------------------------------------------

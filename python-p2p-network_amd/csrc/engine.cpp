@@ -68,8 +68,8 @@ struct p2pg_engine {
   unsigned long long* h_seg_cnt = nullptr;  // pinned
   bool begun = false;                 // p2pg_step_begin ran this round's phase 0
   bool last_push_e = false;    // gossip: pushes of the previous round went to E (dense)
-  double e_thresh = -1.0;      // store-mode when active words >= thresh * active rows * W;
-                               // default (< 0) by row width, see alloc_state
+  double e_thresh = 0.06;      // store-mode when active words >= thresh * active rows * W;
+  double e_thresh_env = -1.0;  // P2PG_E_THRESH (>= 0) or by the current row width (alloc_state)
                                // (c4 A/B, interleaved runs: 0.04 320.4 ms vs 0.1 324.3 ms, round 1;
                                // with the lane-parallel sparse push (round 2) W = 64: 0.04 / 0.06 /
                                // 0.08 -> 278.4 / 275.5 / 275.2 ms, W = 8: 89.1 / 89.4 / 89.5 ms)
@@ -86,6 +86,7 @@ struct p2pg_engine {
   bool frontier_kept = true;   // F[(round-1)&1] holds the last round's first receipts
   bool frontier_kept_prev = true;  // ... and F[round&1] the round before (delivery parents)
   uint64_t prev_aw = 0, prev_av = 0;  // active words / rows of the previous round
+  uint64_t last_new = 0;       // first receipts of the last round run
   int32_t* d_src = nullptr;
   DevState st{};
   size_t plane_bytes = 0, bm_bytes = 0;
@@ -391,7 +392,7 @@ int alloc_state(p2pg_engine* e) {
   free_state(e);
   DevState& s = e->st;
   s.W = e->W;
-  if (e->e_thresh < 0.0) e->e_thresh = e->W > GROUPED_W_MAX ? 0.06 : 0.04;
+  e->e_thresh = e->e_thresh_env >= 0.0 ? e->e_thresh_env : (e->W > GROUPED_W_MAX ? 0.06 : 0.04);
   s.M = e->M;
   e->plane_bytes = (size_t)e->V * e->W * sizeof(uint64_t);
   e->bm_bytes = (size_t)((e->V + 31) / 32) * sizeof(uint32_t);
@@ -460,7 +461,7 @@ int p2pg_create(const p2pg_config* cfg, p2pg_engine** out) {
     return fail(nullptr, P2PG_ERR_ARG, "create: device ordinal out of range");
   p2pg_engine* e = new p2pg_engine;
   e->cfg = *cfg;
-  if (const char* t = std::getenv("P2PG_E_THRESH")) e->e_thresh = std::atof(t);
+  if (const char* t = std::getenv("P2PG_E_THRESH")) e->e_thresh_env = std::atof(t);
   if (const char* t = std::getenv("P2PG_V_THRESH")) e->v_thresh = std::atof(t);
   if (const char* f = std::getenv("P2PG_FUSED")) e->fused = std::strcmp(f, "0") != 0;
   if (const char* f = std::getenv("P2PG_SPARSE_LP")) e->sparse_lp = std::strcmp(f, "0") != 0;
@@ -479,7 +480,12 @@ int p2pg_create(const p2pg_config* cfg, p2pg_engine** out) {
 
 int p2pg_set_stream(p2pg_engine* e, void* hip_stream) {
   if (!e) return P2PG_ERR_ARG;
-  e->stream = hip_stream ? (hipStream_t)hip_stream : e->own_stream;
+  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : e->own_stream;
+  if (s != e->stream && e->stream) {  // work queued on the old stream finishes first
+    HIPCHK(e, hipSetDevice(e->cfg.device));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+  }
+  e->stream = s;
   return P2PG_OK;
 }
 
@@ -669,6 +675,7 @@ int p2pg_reset(p2pg_engine* e) {
   e->total_relays = 0;
   free_arr(e);
   e->prev_aw = e->prev_av = 0;
+  e->last_new = 0;
   for (int i = 0; i < P2PG_KCLASS_N; ++i) {
     e->kms[i] = 0;
     e->klaunch[i] = 0;
@@ -881,6 +888,7 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
   e->total_relays += tot[ST_RELAYS];
   e->prev_aw = tot[ST_ACTIVE_W];
   e->prev_av = tot[ST_ACTIVE_V];
+  e->last_new = tot[ST_NEW];
   e->round += 1;
   if (!active && !(e->cfg.flags & P2PG_FLAG_NO_AUTOSTOP)) e->done = true;
   return active ? 1 : 0;
@@ -915,6 +923,10 @@ int p2pg_get_new_deliveries(p2pg_engine* e, int64_t cap, int32_t* peer, int32_t*
     return fail(e, P2PG_ERR_ARG, "get_new_deliveries: bad arguments");
   if (!e->have_state || e->round == 0)
     return fail(e, P2PG_ERR_STATE, "get_new_deliveries: no round has run");
+  if (e->last_new == 0) {  // a round without receipts has no deliveries (and needs no parents)
+    *n_out = 0;
+    return P2PG_OK;
+  }
   if (!e->frontier_kept || !e->frontier_kept_prev)
     return fail(e, P2PG_ERR_STATE, "get_new_deliveries: the last rounds' frontiers were not kept");
   HIPCHK(e, hipSetDevice(e->cfg.device));
@@ -1017,6 +1029,7 @@ int p2pg_set_exchange(p2pg_engine* e, int64_t n_send, const int32_t* send_local,
   if (!e || !e->d_rowptr || n_send < 0 || n_recv < 0 || (n_send && !send_local) ||
       (n_recv && !recv_local))
     return fail(e, P2PG_ERR_ARG, "set_exchange: bad arguments");
+  if (e->begun) return fail(e, P2PG_ERR_STATE, "set_exchange: a round has begun (step_begin)");
   for (int64_t i = 0; i < n_send; ++i)
     if (send_local[i] < 0 || send_local[i] >= e->V) return fail(e, P2PG_ERR_ARG, "set_exchange: send id out of range");
   for (int64_t i = 0; i < n_recv; ++i)
@@ -1082,6 +1095,7 @@ int p2pg_exchange_pack_live(p2pg_engine* e, int32_t plane, void* dev_buf, int64_
   if (!e || !e->have_state || e->round == 0 || (plane != 0 && plane != 1) || !dev_buf || !counts)
     return fail(e, P2PG_ERR_STATE, "exchange_pack_live: need a completed round, plane 0 or 1, buffers");
   if (!e->d_seg_cnt) return fail(e, P2PG_ERR_STATE, "exchange_pack_live: set_exchange_segments first");
+  if (e->begun) return fail(e, P2PG_ERR_STATE, "exchange_pack_live: the next round has begun");
   if (plane == 1 && e->cfg.mode != P2PG_MODE_GOSSIP)
     return fail(e, P2PG_ERR_ARG, "exchange_pack_live: plane 1 is for gossip pushes");
   HIPCHK(e, hipSetDevice(e->cfg.device));
@@ -1130,6 +1144,7 @@ int p2pg_exchange_unpack_live(p2pg_engine* e, int32_t plane, const void* dev_buf
 static int exchange(p2pg_engine* e, int32_t plane, bool pack, void* buf) {
   if (!e || !e->have_state || e->round == 0 || (plane != 0 && plane != 1))
     return fail(e, P2PG_ERR_STATE, "exchange: need a completed round and plane 0 or 1");
+  if (e->begun) return fail(e, P2PG_ERR_STATE, "exchange: the next round has begun");
   if (plane == 1 && e->cfg.mode != P2PG_MODE_GOSSIP)
     return fail(e, P2PG_ERR_ARG, "exchange: plane 1 is for gossip pushes");
   HIPCHK(e, hipSetDevice(e->cfg.device));
@@ -1161,6 +1176,7 @@ int p2pg_update_edges(p2pg_engine* e, int64_t n_add, const int32_t* add, int64_t
     return fail(e, P2PG_ERR_STATE, "update_edges: not supported on a vertex-partitioned rank");
   if (e->arr_round >= 0 && e->arr_round == e->round)
     return fail(e, P2PG_ERR_STATE, "update_edges: one update per round boundary");
+  if (e->begun) return fail(e, P2PG_ERR_STATE, "update_edges: a round has begun (step_begin)");
   const int64_t V = e->V;
   const std::vector<int64_t>& rp = e->h_rowptr;
   const std::vector<int32_t>& ci = e->h_colidx;
@@ -1362,6 +1378,7 @@ int p2pg_snapshot_size(p2pg_engine* e, int64_t* bytes) {
 int p2pg_snapshot(p2pg_engine* e, void* buf, int64_t cap) {
   if (!e || !buf) return fail(e, P2PG_ERR_ARG, "snapshot: bad arguments");
   if (!e->have_state) return fail(e, P2PG_ERR_STATE, "snapshot: no sources set");
+  if (e->begun) return fail(e, P2PG_ERR_STATE, "snapshot: a round has begun (step_begin)");
   if (e->arr_round >= 0 && e->arr_round == e->round)
     return fail(e, P2PG_ERR_STATE, "snapshot: take it before a topology update or after the next round");
   if (!e->frontier_kept)
@@ -1414,6 +1431,7 @@ int p2pg_snapshot(p2pg_engine* e, void* buf, int64_t cap) {
 int p2pg_restore(p2pg_engine* e, const void* buf, int64_t size) {
   if (!e || !buf || size < (int64_t)sizeof(SnapHeader)) return fail(e, P2PG_ERR_ARG, "restore: bad arguments");
   if (!e->have_state) return fail(e, P2PG_ERR_STATE, "restore: set the same sources first");
+  if (e->begun) return fail(e, P2PG_ERR_STATE, "restore: a round has begun (step_begin)");
   SnapHeader h;
   std::memcpy(&h, buf, sizeof(h));
   if (h.magic != SNAP_MAGIC || h.version != SNAP_VERSION)

@@ -215,7 +215,7 @@ class CompatNetwork:
         rp, ci = graph.rowptr, graph.colidx
         self._link_all((a, int(b)) for a in range(graph.V) for b in ci[rp[a]:rp[a + 1]] if b > a)
         self._deg = graph.degree()
-        self._pending = {}   # {(min, max): connect?} queued for the next round boundary
+        self._pending = {}   # {(min, max): (connect?, dialler, other)} for the next round boundary
         make = engine_factory or GraphNetwork
         self.engine = make(graph, mode=mode, fanout=fanout, **engine_kw)
         self.origins, self.payloads = [], []
@@ -244,16 +244,17 @@ class CompatNetwork:
         return self._by_addr.get((host, port))
 
     def _is_linked(self, a, b):
-        key = (min(a, b), max(a, b))
-        return self._pending.get(key, b in self._links[a])
+        q = self._pending.get((min(a, b), max(a, b)))
+        return q[0] if q is not None else b in self._links[a]
 
     def _queue_change(self, a, b, connect):
-        """Latest request per pair wins; a request that restores the current state cancels."""
+        """Latest request per pair wins; a request that restores the current state cancels.
+        A connect remembers who asked: a is the dialler (outbound end, node.py:122-176)."""
         key = (min(a, b), max(a, b))
         if connect == (b in self._links[a]):
             self._pending.pop(key, None)
         else:
-            self._pending[key] = connect
+            self._pending[key] = (connect, a, b)
 
     def _apply_changes(self):
         """Hand the queued changes to the engine (p2pg_update_edges), then mirror them on the
@@ -262,8 +263,8 @@ class CompatNetwork:
         if not self._pending:
             return
         changes, self._pending = self._pending, {}
-        add = sorted(k for k, c in changes.items() if c)
-        rem = sorted(k for k, c in changes.items() if not c)
+        add = [(a, b) for _, (c, a, b) in sorted(changes.items()) if c]  # (dialler, other)
+        rem = sorted(k for k, (c, _, _) in changes.items() if not c)
         self.engine.update_edges(add=add, remove=rem)
         self.graph = self.engine.graph
         self._deg = self.graph.degree()

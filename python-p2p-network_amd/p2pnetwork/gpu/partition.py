@@ -27,6 +27,8 @@ import numpy as np
 from .graph import PeerGraph
 from .network import GraphNetwork, RoundStats, STAT_FIELDS
 
+MAX_RANKS = 16  # exchange segments per engine (P2PG_MAX_RANKS, csrc/internal.h)
+
 
 class VertexPartition:
     """Contiguous peer ranges balanced by directed-connection count; rank-local CSR."""
@@ -100,9 +102,13 @@ class TorchTransport:
     they are staged through host memory (CPU tests, or ranks sharing one GPU).
 
     * ``exchange_counts(vec)``: all-gather of one small int64 vector per rank (each rank's
-      record count per destination + its round counters) -> [world, len];
+      record count per destination + its round counters) -> [world, len].  The vector is on the
+      host already (the pack reads its counts back), so it goes over a host (gloo) group: no
+      device round trip, no stream synchronisation;
     * ``exchange_records(...)``: grouped point-to-point sends / receives of the packed records
-      (``batch_isend_irecv``), exactly the live rows each peer rank needs."""
+      (``batch_isend_irecv``), exactly the live rows each peer rank needs;
+    * ``engine_stream()``: the stream the rank's engine should launch on (device runs), so
+      that the receives can be ordered before the unpack by a stream wait, not a host sync."""
 
     def __init__(self, device=None, group=None):
         import torch
@@ -112,16 +118,25 @@ class TorchTransport:
         self.device = device
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
+        # counts travel host-side; with RCCL that needs a gloo group next to the nccl one
+        # (a collective call: every rank constructs its transport at the same point)
+        self.host_group = group if self.backend == "gloo" else dist.new_group(
+            ranks=list(range(self.world)) if group is None else dist.get_process_group_ranks(group),
+            backend="gloo")
         self.rows_total = 0  # boundary rows offered / actually sent (exchange volume)
         self.rows_sent = 0
 
+    def engine_stream(self):
+        if self.device is None or not str(self.device).startswith("cuda"):
+            return None
+        return self.torch.cuda.Stream(device=self.device)
+
     def exchange_counts(self, vec):
         torch, dist = self.torch, self.dist
-        dev = self.device if self.backend == "nccl" else "cpu"
-        t = torch.as_tensor(np.asarray(vec, dtype=np.int64), device=dev)
-        out = torch.empty(self.world * t.numel(), dtype=torch.int64, device=dev)
-        dist.all_gather_into_tensor(out, t, group=self.group)
-        return out.cpu().numpy().reshape(self.world, -1)
+        t = torch.as_tensor(np.asarray(vec, dtype=np.int64))
+        out = torch.empty(self.world * t.numel(), dtype=torch.int64)
+        dist.all_gather_into_tensor(out, t, group=self.host_group)
+        return out.numpy().reshape(self.world, -1)
 
     def exchange_records(self, send_buf, send_off, send_cnt, recv_buf, recv_cnt, R):
         """send_buf: records to rank q at record send_off[q], send_cnt[q] of them; recv_buf:
@@ -162,6 +177,8 @@ class PartitionedNetwork:
     def __init__(self, graph, world, rank, transport, mode="flood", fanout=3, gossip_seed=0x5EED,
                  churn_threshold_value=0, churn_seed=0xC0FFEE, record=False, timing=False,
                  device=0, engine_factory=None, overlap=True):
+        if not 1 <= world <= MAX_RANKS:
+            raise ValueError(f"vertex partition over {world} ranks: the exchange supports 1..{MAX_RANKS}")
         if record and mode == "gossip" and world > 1:
             # a gossip parent check needs the REMOTE sender's degree and adjacency order
             raise NotImplementedError("record=True for partitioned gossip: record on one GPU")
@@ -176,6 +193,13 @@ class PartitionedNetwork:
                         churn_threshold_value=churn_threshold_value, churn_seed=churn_seed,
                         record=record, timing=timing, device=device, autostop=False,
                         local_graph=True)
+        # device runs: the engine launches on a torch stream of its own, so the receives (torch's
+        # current stream, which RCCL orders after its transfers) are ordered before the unpack by
+        # a stream wait (_ready), and the next round's interior peers still overlap the transfers
+        st = getattr(transport, "engine_stream", None)
+        self._stream = st() if st is not None else None
+        if self._stream is not None:
+            self.net.set_stream(self._stream.cuda_stream)
         self.net.set_global_ids(self.part.gid)
         self.net.set_exchange(self.part.send_local, self.part.recv_local)
         self.net.set_exchange_segments(self.part.send_counts, self.part.recv_counts)
@@ -217,13 +241,15 @@ class PartitionedNetwork:
                           wedges=int(deg[words // W].sum()), deg_active=int(deg[vs].sum()),
                           scatter_words=0, touched_words=0)
 
-    @staticmethod
-    def _ready(t):
+    def _ready(self, t):
         """Records received with torch ops / RCCL are ordered on torch's current stream; the
-        engine unpacks on its own stream, so wait for them first (nothing else orders them)."""
+        engine unpacks on its own stream, which waits for them on the device (no host sync)."""
         if getattr(t, "is_cuda", False):
             import torch
-            torch.cuda.current_stream(t.device).synchronize()
+            if self._stream is None:  # an engine on a stream torch does not know: host sync
+                torch.cuda.current_stream(t.device).synchronize()
+            else:
+                self._stream.wait_stream(torch.cuda.current_stream(t.device))
         return t
 
     def step(self):

@@ -219,3 +219,40 @@ def test_compat_repeated_disconnect_is_queued_once():
     assert events.count(("inbound_node_disconnected", "1")) == 1
     assert events.count(("outbound_node_disconnected", "0")) == 1
     assert [c.id for c in net.nodes[1].all_nodes] == ["2"]
+
+
+def test_compat_higher_id_dialler_is_the_outbound_end():
+    """Peer 5 dials peer 2 (connect_with_node, node.py:122-176): 5 holds the outbound handle and
+    sees outbound_node_connected, 2 the inbound one -- whatever the id order -- and 5 can later
+    close it with disconnect_with_node (it is in 5's nodes_outbound, node.py:178-189)."""
+    from p2pnetwork.gpu import PeerGraph
+    from p2pnetwork.gpu.compat import CompatNetwork, SimNode
+    events = []
+
+    def cb(event, main_node, connected_node, data):
+        events.append((event, main_node.id, getattr(connected_node, "id", None)))
+
+    class Eng(MockEngine):
+        updates = []
+
+        def update_edges(self, add=(), remove=()):
+            Eng.updates.append((list(add), list(remove)))
+            self.graph = self.g = self.g.with_changes(add, remove)
+
+    g = PeerGraph.from_edges(6, [(0, 1), (1, 2), (3, 4)])
+    net = CompatNetwork(g, SimNode, node_kwargs={"callback": cb}, engine_factory=Eng)
+    events.clear()
+    n2, n5 = net.nodes[2], net.nodes[5]
+    assert n5.connect_with_node(n2.host, n2.port)
+    net._apply_changes()
+    assert events == [("outbound_node_connected", "5", "2"), ("inbound_node_connected", "2", "5")]
+    assert [c.id for c in n5.nodes_outbound] == ["2"] and n5.nodes_inbound == []
+    assert [c.id for c in n2.nodes_inbound] == ["1", "5"]
+    events.clear()
+    n5.disconnect_with_node(n5.nodes_outbound[0])
+    net._apply_changes()
+    assert Eng.updates[-1] == ([], [(2, 5)])
+    assert ("node_disconnect_with_outbound_node", "5", "2") in events
+    assert ("outbound_node_disconnected", "5", "2") in events
+    assert ("inbound_node_disconnected", "2", "5") in events
+    assert n5.all_nodes == [] and [c.id for c in n2.all_nodes] == ["1"]

@@ -177,3 +177,60 @@ def test_run_chunks_keep_the_last_frontier(M):
                 break
         assert fused_cuts >= 2
         np.testing.assert_array_equal(a.seen_plane(), b.seen_plane())
+
+
+def test_quiescent_run_after_unstored_fused_round(monkeypatch):
+    """p2pg_run to quiescence with every gossip round in edge form (P2PG_GOSSIP_PUSH=store): the
+    last round with receipts is fused and, being more than two rounds before max_rounds, does
+    not store its frontier; the quiescent round after it has no deliveries and needs no parents,
+    so deliveries() is empty (not an error) and a snapshot can be taken."""
+    from p2pnetwork.gpu import GraphNetwork, PeerGraph, make_sources
+    monkeypatch.setenv("P2PG_GOSSIP_PUSH", "store")
+    g = PeerGraph.random_regular(3000, 8, seed=2)
+    src = make_sources(g.V, 256, seed=2)
+    with GraphNetwork(g, mode="gossip", fanout=3, gossip_seed=GSEED) as a, \
+            GraphNetwork(g, mode="gossip", fanout=3, gossip_seed=GSEED) as b:
+        a.broadcast(src)
+        b.broadcast(src)
+        rounds = a.run()
+        assert not rounds[-1].active and rounds[-2].push_form == 3 and rounds[-2].new_deliveries > 0
+        d = a.deliveries()
+        assert len(d) == 0
+        assert len(a.snapshot()) > 0
+        step = []
+        while True:
+            step.append(b.step())
+            if not step[-1].active:
+                break
+        assert [r.as_dict() for r in rounds] == [r.as_dict() for r in step]
+        np.testing.assert_array_equal(a.seen_plane(), b.seen_plane())
+
+
+def test_config3_full_size_matches_c_oracle():
+    """Config 3 itself (1M-peer G(n,p) mean degree 16, 4096 concurrent floods) against
+    oracle/relay_oracle.c at full size: the whole seen plane (all 4096 broadcasts) and every
+    per-round counter; then words 0 and 63 as 64-broadcast runs with their global message ids,
+    whose first-receipt round and lowest-id sender planes (1M x 64 each) equal the oracle's bit
+    for bit and whose seen word equals the 4096-run's.  Anchor: node.py:106-120."""
+    from p2pnetwork.gpu import GraphNetwork, PeerGraph, make_sources
+    g = PeerGraph.gnp(1_000_000, 16, seed=1)
+    src = make_sources(g.V, 4096, seed=1)
+    with GraphNetwork(g, mode="flood") as net:
+        net.broadcast(src)
+        rounds = net.run()
+        seen = net.seen_plane()
+    ora = coracle.run(g.rowptr, g.colidx, src, "flood", record=False, want_seen=True)
+    np.testing.assert_array_equal(seen, ora.seen)
+    assert_rounds_equal(rounds, ora.rounds)
+    del ora
+    for w in (0, 63):
+        s64 = src[64 * w:64 * w + 64]
+        with GraphNetwork(g, mode="flood", record=True, msg_id_base=64 * w) as sub:
+            sub.broadcast(s64)
+            r = sub.run()
+            hop, par = sub.hop_parent()
+            np.testing.assert_array_equal(sub.seen_word(0), seen[:, w])
+        o = coracle.run(g.rowptr, g.colidx, s64, "flood", record=True)
+        assert_rounds_equal(r, o.rounds)
+        assert np.array_equal(hop, o.hop), f"word {w}: hop planes differ"
+        assert np.array_equal(par, o.parent), f"word {w}: parent planes differ"

@@ -29,6 +29,12 @@ class ThreadTransport:
         s["barrier"].wait()
         return items
 
+    def engine_stream(self):
+        # as TorchTransport on a GPU: the engine gets a torch stream, and the unpack waits for
+        # the copies below by a stream wait (PartitionedNetwork._ready), not a host sync
+        import torch
+        return torch.cuda.Stream(device=0)
+
     def exchange_counts(self, vec):
         return np.stack(self._gather(np.asarray(vec, dtype=np.int64)))
 

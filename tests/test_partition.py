@@ -1,5 +1,5 @@
 """Vertex-partitioned multi-GPU path (p2pnetwork.gpu.partition), exercised on CPU with the
-gloo backend (world size 2 and 3) through the real orchestration code; each rank's engine is
+gloo backend (world sizes 2, 3 and 8) through the real orchestration code; each rank's engine is
 the test-only NumPy stand-in of tests/partition_mock.py.  The union of the ranks' owned
 results must equal the single-graph oracle bit for bit (hop, parent, per-round counters)."""
 import os
@@ -90,6 +90,10 @@ def _rank_main(rank, world, port, kind, mode, M, thr, out, overlap=True):
     ("ba", "gossip", 64, 0, 2, True),
     ("ba", "gossip", 64, 0, 2, False),
     ("ws", "gossip", 30, 500_000_000, 3, True),
+    # the 8 ranks config 5 runs on one node
+    ("ws", "flood", 70, 300_000_000, 8, True),
+    ("ba", "gossip", 64, 0, 8, True),
+    ("ws", "gossip", 96, 200_000_000, 8, False),
 ])
 def test_partitioned_gloo_matches_oracle(kind, mode, M, thr, world, overlap):
     """Ranks over gloo (stand-in engines) == the oracle, with the compacted record exchange
@@ -124,3 +128,11 @@ def test_partitioned_gloo_matches_oracle(kind, mode, M, thr, world, overlap):
     np.testing.assert_array_equal(trim_zeros(r0["new"]), trim_zeros([r["new_deliveries"] for r in ora.rounds]))
     np.testing.assert_array_equal(trim_zeros(r0["words"]), trim_zeros([r["active_words"] for r in ora.rounds]))
     np.testing.assert_array_equal(trim_zeros(r0["scatter"]), trim_zeros([r["scatter_words"] for r in ora.rounds]))
+
+
+def test_partition_refuses_more_ranks_than_the_exchange_holds():
+    from p2pnetwork.gpu import PartitionedNetwork
+    from partition_mock import MockEngine
+    g = make_graph("ws")
+    with pytest.raises(ValueError, match="1..16"):
+        PartitionedNetwork(g, 17, 0, transport=None, engine_factory=MockEngine)
