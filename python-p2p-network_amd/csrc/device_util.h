@@ -211,6 +211,35 @@ __device__ __forceinline__ uint32_t select_bit64(uint64_t x, uint32_t n) {
   return (up ? 32u : 0u) + select_bit32(up ? (uint32_t)(x >> 32) : lo, up ? n - cl : n);
 }
 
+// Word-major list of the set bits of every lane's 64-bit word f (the gossip pick lists, DESIGN.md
+// 4a): the r-th set bit b of lane l's word becomes entry (tag | b) at position li0 + r, li0 = the
+// lane's exclusive prefix of popcounts minus the entries of earlier passes (wrapping: positions
+// below the pass are never written); positions >= cap belong to a later pass.  Entries that are
+// not written go to lst[dummy] (one address for all lanes: an LDS broadcast, no bank conflict).
+// Two entries per lane per trip -- the r-th bit of each 32-bit half, the high half's entries
+// following the low half's -- and a wave-uniform trip count (the largest half popcount), so the
+// loop has no divergence and no exec-mask bookkeeping (the per-bit loop it replaces ran the low
+// and the high half one after the other, ~17 instructions per bit, with lanes dropping out).
+__device__ __forceinline__ void list_bits(uint16_t* lst, uint32_t dummy, uint64_t f, uint32_t tag,
+                                          uint32_t li0, uint32_t cap) {
+  uint32_t lo = (uint32_t)f, hi = (uint32_t)(f >> 32);
+  const uint32_t pl = (uint32_t)__popc(lo), ph = (uint32_t)__popc(hi);
+  const uint32_t trips = wave_reduce_u32<true>(pl > ph ? pl : ph);
+  uint32_t al = li0, ah = li0 + pl;
+  const uint32_t th = tag | 32u;
+  for (uint32_t t = 0; t < trips; ++t) {
+    // (bit 31 forced on: a defined ctz when the half is empty -- that entry goes to the dummy)
+    const uint32_t bl = (uint32_t)__builtin_ctz(lo | 0x80000000u);
+    const uint32_t bh = (uint32_t)__builtin_ctz(hi | 0x80000000u);
+    lst[(t < pl && al < cap) ? al : dummy] = (uint16_t)(tag | bl);
+    lst[(t < ph && ah < cap) ? ah : dummy] = (uint16_t)(th | bh);
+    lo &= lo - 1u;
+    hi &= hi - 1u;
+    ++al;
+    ++ah;
+  }
+}
+
 // Orders this wave's LDS writes before its later LDS reads by other lanes.
 __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");

@@ -80,6 +80,8 @@ struct p2pg_engine {
   bool fused = true;           // dense rounds after dense rounds: one pull+scatter pass
   bool wide_atomic = true;     // fused rounds: hub pushes by atomics (P2PG_WIDE_ATOMIC=0: one
                                // wave per 16-connection chunk item)
+  int push_dedup = -1;         // sparse pushes drop seen bits: -1 in the decay phase, 0 never,
+                               // 1 always (P2PG_PUSH_DEDUP)
   bool sparse_lp = true;       // sparse rounds: lane-parallel scatter (relay_sparse.hip) when
                                // the rows allow it; P2PG_SPARSE_LP=0 keeps the per-source one
   bool skip_frontier = false;  // p2pg_run, not its last two allowed rounds: fused rounds may skip F
@@ -254,6 +256,7 @@ RoundParams params(const p2pg_engine* e) {
   p.border = nullptr;
   p.phase = -1;
   p.store_f = 1;
+  p.dedup_push = 0;
   return p;
 }
 
@@ -465,6 +468,7 @@ int p2pg_create(const p2pg_config* cfg, p2pg_engine** out) {
   if (const char* t = std::getenv("P2PG_V_THRESH")) e->v_thresh = std::atof(t);
   if (const char* f = std::getenv("P2PG_FUSED")) e->fused = std::strcmp(f, "0") != 0;
   if (const char* f = std::getenv("P2PG_SPARSE_LP")) e->sparse_lp = std::strcmp(f, "0") != 0;
+  if (const char* f = std::getenv("P2PG_PUSH_DEDUP")) e->push_dedup = std::atoi(f);
   if (const char* f = std::getenv("P2PG_WIDE_ATOMIC")) e->wide_atomic = std::strcmp(f, "0") != 0;
   if (const char* m = std::getenv("P2PG_GOSSIP_PUSH"))
     e->push_mode = !std::strcmp(m, "atomic") ? 1 : (!std::strcmp(m, "store") ? 2 : 0);
@@ -845,6 +849,10 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
     }
     // the lane-parallel sparse push sizes its (peer, word) list by the frontier's word count
     if (!use_e && !have_tot && sparse_scatter_on(e) && (rc = read_stats())) return rc;
+    // decay phase (fewer first receipts than the round before): most pushes are duplicates,
+    // so the sparse push drops seen bits before its atomics (RoundParams::dedup_push)
+    if (!use_e && sparse_scatter_on(e))
+      p.dedup_push = e->push_dedup == 1 || (e->push_dedup < 0 && tot[ST_NEW] < e->last_new);
     if ((rc = timed(e, use_e ? 6 : 2, [&] {
            return use_e ? launch_gossip_scatter(g, s, p, e->d_hub, e->n_hub, true, e->stream,
                                                 e->d_hub_big, e->n_hub_big, e->d_wide_big,

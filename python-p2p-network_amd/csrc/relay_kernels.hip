@@ -1055,17 +1055,14 @@ __device__ __forceinline__ void scatter_row(const DevGraph& g, const DevState& s
     const uint32_t incl = wave_scan_u32(cnt);
     const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     const uint32_t pos0 = incl - cnt;
-    for (uint32_t lb = 0; lb < total; lb += GLIST) {
-      const uint32_t nw = total - lb < (uint32_t)GLIST ? total - lb : (uint32_t)GLIST;
-      uint32_t li = pos0 - lb;  // list index of this lane's next bit (wraps below the pass)
-      const uint32_t hi_tag = ((uint32_t)lane << 6) | 32u;
-      for (uint32_t h = (uint32_t)f; h; h &= h - 1u, ++li)
-        if (li < nw) L.lst[li] = (uint16_t)(((uint32_t)lane << 6) | (uint32_t)__builtin_ctz(h));
-      for (uint32_t h = (uint32_t)(f >> 32); h; h &= h - 1u, ++li)
-        if (li < nw) L.lst[li] = (uint16_t)(hi_tag | (uint32_t)__builtin_ctz(h));
+    // a pass lists GLIST - 1 entries; the last list slot takes the entries not written
+    constexpr uint32_t CAP = (uint32_t)GLIST - 1u;
+    for (uint32_t lb = 0; lb < total; lb += CAP) {
+      const uint32_t nw = total - lb < CAP ? total - lb : CAP;
+      list_bits(L.lst, CAP, f, (uint32_t)lane << 6, pos0 - lb, nw);
       wave_lds_sync();
       PROF_MARK(6);
-      const uint32_t n = total - lb < (uint32_t)GLIST ? total - lb : (uint32_t)GLIST;
+      const uint32_t n = nw;
       if constexpr (K > 0) {
         // a source whose whole adjacency is this chunk needs no range check on its picks
         if (nb == 0 && nn == (int)deg)

@@ -271,9 +271,13 @@ __global__ __launch_bounds__(256) void k_sparse_push(DevGraph g, DevState st, Ro
           if (CHURN && churn_dropped((uint32_t)p.round, gv, gidx(g, v), p.churn_thr, p.cseed_lo,
                                      p.cseed_hi))
             continue;
+          pushed += 1;  // a distinct (sender, target, word) mask, counted before the dedup
+          if (p.dedup_push) {
+            mask &= ~st.seen[(int64_t)v * W + gw];
+            if (!mask) continue;  // a duplicate in its entirety: nothing to deliver
+          }
           atomicOr((unsigned long long*)&nx[(int64_t)v * W + gw], (unsigned long long)mask);
           touched[v] = 1u;  // a plain byte store: a T-bitmap atomic here doubled the atomics
-          pushed += 1;
         }
       }
       wave_lds_sync();  // the entries' LDS is rewritten by the next pass

@@ -6,9 +6,16 @@ tag=$1; msgs=$2; reps=$3; shift 3
 mkdir -p gpurun_out/$tag
 for rep in $(seq 1 $reps); do
   for v in "$@"; do
-    lib=""; [ "$v" != default ] && lib=python-p2p-network_amd/csrc/variants/$v/libp2pgpu.so
-    f=gpurun_out/$tag/m${msgs}_${v}_$rep.json
-    P2PG_LIB=$lib timeout -k 10 180 python bench.py --steps 5 --warmup 1 --msgs $msgs --no-cpu-baseline > $f 2> $f.err || { tail -20 $f.err; exit 1; }
+    # variant: "default" (in-tree build), a variants/<v> build, or "env:NAME=VAL[,NAME=VAL]"
+    # (the in-tree build under runtime knobs)
+    lib=""; envs=""
+    case "$v" in
+      default) ;;
+      env:*) envs=$(echo "${v#env:}" | tr ',' ' ') ;;
+      *) lib=python-p2p-network_amd/csrc/variants/$v/libp2pgpu.so ;;
+    esac
+    f=gpurun_out/$tag/m${msgs}_$(echo "$v" | tr ':=,' '___')_$rep.json
+    env P2PG_LIB=$lib $envs timeout -k 10 180 python bench.py --steps 5 --warmup 1 --msgs $msgs --no-cpu-baseline > $f 2> $f.err || { tail -20 $f.err; exit 1; }
     python3 - "$f" "$v" <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
