@@ -73,7 +73,8 @@ struct p2pg_engine {
                                // (c4 A/B, interleaved runs: 0.04 320.4 ms vs 0.1 324.3 ms, round 1;
                                // with the lane-parallel sparse push (round 2) W = 64: 0.04 / 0.06 /
                                // 0.08 -> 278.4 / 275.5 / 275.2 ms, W = 8: 89.1 / 89.4 / 89.5 ms)
-  double v_thresh = 0.3;       // ... and active rows >= v_thresh * V: a dense round visits every
+  double v_thresh = 0.3;       // ... and active rows >= v_thresh * V (by row width, alloc_state;
+  double v_thresh_env = -1.0;  // P2PG_V_THRESH overrides): a dense round visits every
                                // unsaturated peer, a sparse one only the pushed-to rows (narrow
                                // rows: word density alone is high whenever anything is active)
   int push_mode = 0;           // 0 auto, 1 always row atomics, 2 always edge stores
@@ -396,6 +397,13 @@ int alloc_state(p2pg_engine* e) {
   DevState& s = e->st;
   s.W = e->W;
   e->e_thresh = e->e_thresh_env >= 0.0 ? e->e_thresh_env : (e->W > GROUPED_W_MAX ? 0.06 : 0.04);
+  // a dense round costs a visit of every unsaturated peer whatever the width, a sparse one an
+  // atomic per pushed mask: narrow rows (a message split's shares) stay sparse until nearly every
+  // peer is active (c4 interleaved sweeps, profiles/r03/ab_v_thresh.txt: W = 8 0.3 / 0.6 / 0.9 /
+  // 0.95 / 0.98 -> 85.6 / 81.3 / 79.9 / 79.2 / 83.6 ms; W = 16 -> 144.5 / 138.9 / 130.4 / 128.7 /
+  // 127.6 ms; W = 32 0.3 / 0.7 / 0.9 / 0.95 -> 218.4 / 211.7 / 208.4 / 203.7 ms; W = 64: 0.3 ...
+  // 0.9 equal, 0.95 within 1 %, so the round-2 value stays)
+  e->v_thresh = e->v_thresh_env >= 0.0 ? e->v_thresh_env : e->W <= 32 ? 0.95 : 0.3;
   s.M = e->M;
   e->plane_bytes = (size_t)e->V * e->W * sizeof(uint64_t);
   e->bm_bytes = (size_t)((e->V + 31) / 32) * sizeof(uint32_t);
@@ -465,7 +473,7 @@ int p2pg_create(const p2pg_config* cfg, p2pg_engine** out) {
   p2pg_engine* e = new p2pg_engine;
   e->cfg = *cfg;
   if (const char* t = std::getenv("P2PG_E_THRESH")) e->e_thresh_env = std::atof(t);
-  if (const char* t = std::getenv("P2PG_V_THRESH")) e->v_thresh = std::atof(t);
+  if (const char* t = std::getenv("P2PG_V_THRESH")) e->v_thresh_env = std::atof(t);
   if (const char* f = std::getenv("P2PG_FUSED")) e->fused = std::strcmp(f, "0") != 0;
   if (const char* f = std::getenv("P2PG_SPARSE_LP")) e->sparse_lp = std::strcmp(f, "0") != 0;
   if (const char* f = std::getenv("P2PG_PUSH_DEDUP")) e->push_dedup = std::atoi(f);

@@ -42,8 +42,8 @@ struct GroupedLds {
   alignas(8) uint32_t tbl[TS][WP][2];  // (slot, word) mask as two 32-bit halves (LDS atomics)
   uint16_t lst[GLIST_G];               // new bits: lane << 6 | bit
   int32_t off[36];                     // batch peer i -> first slot of its row, batch-relative
-  uint32_t wmask[32];                  // batch peer i -> active words of its new frontier row
-  uint8_t owner[64];                   // pick-window slot -> batch peer
+  uint32_t swm[64];                    // pick-window slot -> active words of its peer's new row
+  uint8_t owner[64];                   // pick-window slot -> batch peer (churn only)
 };
 
 // lane-varying read of lane src's 64-bit value
@@ -150,8 +150,12 @@ __global__ __launch_bounds__(256, P2PG_GROUPED_WAVES) void k_gossip_fused_groupe
       const bool mine = gl < n && ((todo >> (b0 + gl)) & 1u);
       // PO: the peer's frontier row (its new receipts) instead of its seen row
       if (mine && wvalid) q.s = ld_once(&(PO ? Fc : st.seen)[(u0 + b0 + gl) * W + wl]);
-      int gj = 0;  // batch peer owning slot rb0 + lane
-      for (int i = 1; i < n; ++i) gj += readlane64(rp, b0 + i) - rb0 <= (int64_t)lane;
+      // batch peer owning slot rb0 + lane: the number of later row starts at or below it
+      // (32-bit offsets relative to the batch; a batch spans <= TS slots or one peer)
+      const uint32_t rel = (uint32_t)(rp - rb0);
+      int gj = 0;
+      for (int i = 1; i < n; ++i)
+        gj += (uint32_t)__builtin_amdgcn_readlane((int)rel, b0 + i) <= (uint32_t)lane;
       q.rcv = rb0 + lane < q.rb1 && ((todo >> (b0 + gj)) & 1u);
       if (q.rcv) {
         q.v = ld_once(&g.colidx[rb0 + lane]);
@@ -221,11 +225,11 @@ __global__ __launch_bounds__(256, P2PG_GROUPED_WAVES) void k_gossip_fused_groupe
       for (int s0 = 0; s0 < ns; s0 += SPI) {
         const int sl = s0 + gl;
         const bool ok = sl < ns && wvalid;
-        const int o = ok ? L.owner[sl] : 0;
-        const uint32_t wmk = ok ? L.wmask[o] : 0u;
+        const uint32_t wmk = ok ? L.swm[sl] : 0u;
         const int js = p0 + sl;  // batch slot
         uint32_t rv = bperm(js & 63, q.rv);
         int32_t tv = CHURN ? (int32_t)bperm(js & 63, (uint32_t)q.v) : 0;
+        const int o = CHURN ? (int)L.owner[sl < ns ? sl : 0] : 0;  // churn: the sending peer
         // packed: the sender's active words, in order; else every word of an active sender
         if (packed ? ((wmk >> wl) & 1u) != 0u : (wmk != 0u && wvalid)) {
           if (js >= 64) {  // beyond the registers (one peer wider than 64 slots)
@@ -318,7 +322,6 @@ __global__ __launch_bounds__(256, P2PG_GROUPED_WAVES) void k_gossip_fused_groupe
       const uint32_t gi = lane < n ? (uint32_t)((wm_all >> (lane * WP)) & gmask) : 0u;
       if (!wm_all) return;
       // 4. this round's pushes: picks into the (slot, word) table, then the flush
-      if (lane < n) L.wmask[lane] = gi;
       const int32_t rel = (int32_t)(rp - a.rb0);
       if (lane >= a.b0 && lane <= a.b0 + n) L.off[lane - a.b0] = rel;
       const uint32_t cntb = (uint32_t)__popcll(nw);
@@ -329,15 +332,16 @@ __global__ __launch_bounds__(256, P2PG_GROUPED_WAVES) void k_gossip_fused_groupe
       const uint32_t gv_base = (uint32_t)(u0 + a.b0);
       for (int32_t p0 = 0; p0 < nslots; p0 += TS) {
         const int ns = nslots - p0 < TS ? nslots - p0 : TS;
+        // the flush's word mask per window slot: its owner's new words
+        int o = 0;
+        for (int i = 1; i < n; ++i) o += __builtin_amdgcn_readlane(rel, a.b0 + i) <= p0 + lane;
+        const uint32_t swm = bperm(o, gi);
         if (lane < ns) {
-          int o = 0;
-          for (int i = 1; i < n; ++i) o += __builtin_amdgcn_readlane(rel, a.b0 + i) <= p0 + lane;
-          L.owner[lane] = (uint8_t)o;
+          L.swm[lane] = swm;
+          if (CHURN) L.owner[lane] = (uint8_t)o;
         }
-        for (int e = lane; e < ns * WP; e += 64) {
-          L.tbl[e >> LW][e & (WP - 1)][0] = 0u;
-          L.tbl[e >> LW][e & (WP - 1)][1] = 0u;
-        }
+        for (int e = lane; e < ns * WP; e += 64)  // (slot, word) masks, one 64-bit write each
+          reinterpret_cast<uint64_t*>(&L.tbl[0][0][0])[e] = 0ull;
         for (uint32_t lb = 0; lb < total; lb += GLIST_G) {
           const uint32_t ne = total - lb < (uint32_t)GLIST_G ? total - lb : (uint32_t)GLIST_G;
           uint32_t li = pos0 - lb;

@@ -133,6 +133,7 @@ def test_gossip_wide_rows_hubs_churn_match_c_oracle(V, M, fanout, churn, push, m
     from p2pnetwork.gpu.network import churn_threshold
     monkeypatch.setenv("P2PG_GOSSIP_PUSH", "auto")
     monkeypatch.setenv("P2PG_FUSED", "0" if push == "store_unfused" else "1")
+    monkeypatch.setenv("P2PG_V_THRESH", "0.3")  # dense rounds from 30 % active peers on
     g = _hub_graph(V, 4, seed=V + M)
     src = make_sources(g.V, M, seed=7)
     thr = churn_threshold(churn) if churn else 0
@@ -150,11 +151,12 @@ def test_gossip_wide_rows_hubs_churn_match_c_oracle(V, M, fanout, churn, push, m
 
 
 @pytest.mark.parametrize("M", [4096, 512])
-def test_run_chunks_keep_the_last_frontier(M):
+def test_run_chunks_keep_the_last_frontier(M, monkeypatch):
     """p2pg_run drops the frontier rows of fused rounds nobody can observe, but the last round a
     call may run keeps them: runs cut after a fused round give the same deliveries and seen
     plane as round-by-round stepping (W = 64: one peer per wave; W = 8: grouped kernel)."""
     from p2pnetwork.gpu import GraphNetwork, PeerGraph, make_sources
+    monkeypatch.setenv("P2PG_V_THRESH", "0.3")  # dense rounds from 30 % active peers on
     g = PeerGraph.barabasi_albert(200_000, 4, seed=3)
     src = make_sources(g.V, M, seed=3)
     with GraphNetwork(g, mode="gossip", fanout=3, gossip_seed=GSEED) as a, \

@@ -50,9 +50,13 @@ def _check_split(g, M, world, churn=0, bounds=None):
     assert got == want
 
 
-@pytest.mark.parametrize("world", [2, 4, 8])
-def test_message_split_union_equals_one_engine_1m(world):
+@pytest.mark.parametrize("world,vthr", [(2, None), (4, None), (8, None), (4, "0.3"), (8, "0.3")])
+def test_message_split_union_equals_one_engine_1m(world, vthr, monkeypatch):
+    """vthr: the dense-round entry threshold (active peers / V); narrow rows default to 0.95 (few
+    dense rounds), 0.3 runs most rounds through the grouped fused kernel."""
     from p2pnetwork.gpu import PeerGraph
+    if vthr is not None:
+        monkeypatch.setenv("P2PG_V_THRESH", vthr)
     _check_split(PeerGraph.barabasi_albert(1_000_000, 4, seed=3), 4096, world)
 
 
