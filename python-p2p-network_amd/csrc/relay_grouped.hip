@@ -31,6 +31,11 @@ namespace p2pg {
 namespace {
 
 constexpr int GLIST_G = 1024;  // new bits listed per pick pass (a peak-round batch: ~700)
+// E-row gathers per lane issued one batch ahead (and per round trip after that)
+#ifndef P2PG_GFG
+#define P2PG_GFG 6  // c4 A/B (profiles/r03/ab_gfg.txt): W = 8 fused 49.7 -> 47.7 ms, W = 16 97.2 -> 94.1 ms; 8 spills
+#endif
+constexpr int GFG = P2PG_GFG;
 
 template <int LW>
 struct GroupedLds {
@@ -180,10 +185,16 @@ __global__ __launch_bounds__(256, P2PG_GROUPED_WAVES) void k_gossip_fused_groupe
       const int64_t lo = readlane64_v(rp, bi) - cb, hi = readlane64_v(rp, bi + 1) - cb;
       return bits_between(lo < 0 ? 0 : (lo > 64 ? 64 : (int)lo), hi < 0 ? 0 : (hi > 64 ? 64 : (int)hi));
     };
-    uint64_t X[4];
+    uint64_t X[GFG];
+    auto x_or = [&]() {
+      uint64_t o = 0;
+#pragma unroll
+      for (int qq = 0; qq < GFG; ++qq) o |= X[qq];
+      return o;
+    };
     auto gathers = [&](int64_t cb, uint64_t& mg, uint64_t amv) {
 #pragma unroll
-      for (int qq = 0; qq < 4; ++qq) {
+      for (int qq = 0; qq < GFG; ++qq) {
         const bool ok = mg != 0ull;
         const int idx = ok ? __builtin_ctzll(mg) : 0;
         mg &= mg - 1ull;
@@ -209,7 +220,8 @@ __global__ __launch_bounds__(256, P2PG_GROUPED_WAVES) void k_gossip_fused_groupe
     };
     auto first_gathers = [&](GStage& q) {
       q.mr = 0;
-      X[0] = X[1] = X[2] = X[3] = 0ull;
+#pragma unroll
+      for (int qq = 0; qq < GFG; ++qq) X[qq] = 0ull;
       if (PO || q.n == 0) return;
       const uint64_t need = need_of(q);
       const uint64_t am = active_slots(q, q.rb0, q.v, q.rcv, q.aword);
@@ -251,14 +263,14 @@ __global__ __launch_bounds__(256, P2PG_GROUPED_WAVES) void k_gossip_fused_groupe
 
     auto consume = [&](GStage& a, GStage& b, GStage& cc, GStage& d) {
       // 1. arrivals: the first gathers (in flight since the last step) + the rest
-      uint64_t acc = (X[0] | X[1]) | (X[2] | X[3]);
+      uint64_t acc = x_or();
       const uint64_t need = need_of(a);
       if (PO) acc = a.s;  // the frontier row
       if (!PO) {
         uint64_t mg = a.mr;
         while (__ballot(mg != 0ull)) {
           gathers(a.rb0, mg, a.amv);
-          acc |= (X[0] | X[1]) | (X[2] | X[3]);
+          acc |= x_or();
         }
         for (int64_t cb = a.rb0 + 64; cb < a.rb1; cb += 64) {  // one peer wider than 64 slots
           int32_t v = 0;
@@ -275,7 +287,7 @@ __global__ __launch_bounds__(256, P2PG_GROUPED_WAVES) void k_gossip_fused_groupe
           uint64_t m2 = need ? am & ms : 0ull;
           while (__ballot(m2 != 0ull)) {
             gathers(cb, m2, amv);
-            acc |= (X[0] | X[1]) | (X[2] | X[3]);
+            acc |= x_or();
           }
         }
       }
