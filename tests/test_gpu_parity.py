@@ -288,6 +288,30 @@ def test_gpu_gossip_push_forms_match_golden(name, push, monkeypatch):
     assert_rounds_equal(rounds, ora.rounds)
 
 
+@pytest.mark.parametrize("dedup", ["0", "1"])
+@pytest.mark.parametrize("name", golden_cases())
+def test_gpu_sparse_push_dedup_matches_golden(name, dedup, monkeypatch):
+    """Sparse pushes that drop already-seen bits before their atomics (RoundParams::dedup_push;
+    by default only in the decay phase) in EVERY round (1) or none (0), row atomics only: the
+    same deliveries, parents and oracle counters -- the dedup of README.md:20 moves to the
+    sender, it does not change what arrives (scatter_words is counted before the filter)."""
+    z = load_golden(name)
+    if str(z["mode"]) != "gossip":
+        pytest.skip("flood case")
+    monkeypatch.setenv("P2PG_GOSSIP_PUSH", "atomic")
+    monkeypatch.setenv("P2PG_PUSH_DEDUP", dedup)
+    with gpu_net(z, "gossip", int(z["fanout"]), int(z["gossip_seed"]), int(z["churn_threshold"]),
+                 int(z["churn_seed"])) as net:
+        net.broadcast(z["src"])
+        rounds = net.run()
+        hop, parent = net.hop_parent()
+    np.testing.assert_array_equal(hop, z["hop"])
+    np.testing.assert_array_equal(parent, z["parent"])
+    ora = oracle_for(z["rowptr"], z["colidx"], z["src"], "gossip", int(z["fanout"]), int(z["gossip_seed"]),
+                     int(z["churn_threshold"]), int(z["churn_seed"]))
+    assert_rounds_equal(rounds, ora.rounds)
+
+
 @pytest.mark.parametrize("push", ["atomic", "store", "store_unfused"])
 @pytest.mark.parametrize("kind,p,M,thr,fanout", [
     ("hub", dict(V=1500, m=3, star=1100), 64, 0, 3),
