@@ -82,7 +82,11 @@ struct GStage {
 // active peers, their arrivals are their own frontier rows F[r&1] (dedup, counters, bitmaps were
 // done by the update), and only the picks and the flush run (replaces one wave per source with
 // 8 of 64 lanes busy at W = 8).
-template <bool CHURN, int K, int LW, bool PO = false>
+// PL (pull only): the last dense round before the sparse ones -- arrivals gathered from E, dedup,
+// frontier rows and bitmaps as in a fused round, no picks and no flush (the round's pushes go by
+// row atomics afterwards).  The one-peer-per-wave pull (k_pull1) spends a whole wave visit on
+// every peer with 8 of 64 lanes busy at W = 8.
+template <bool CHURN, int K, int LW, bool PO = false, bool PL = false>
 __global__ __launch_bounds__(256, P2PG_GROUPED_WAVES) void k_gossip_fused_grouped(DevGraph g, DevState st, RoundParams p) {
   using Lds = GroupedLds<LW>;
   constexpr int WP = Lds::WP;
@@ -332,7 +336,7 @@ __global__ __launch_bounds__(256, P2PG_GROUPED_WAVES) void k_gossip_fused_groupe
         sat |= (uint32_t)__ballot(done_i) << a.b0;
       }
       const uint32_t gi = lane < n ? (uint32_t)((wm_all >> (lane * WP)) & gmask) : 0u;
-      if (!wm_all) return;
+      if (PL || !wm_all) return;
       // 4. this round's pushes: picks into the (slot, word) table, then the flush
       const int32_t rel = (int32_t)(rp - a.rb0);
       if (lane >= a.b0 && lane <= a.b0 + n) L.off[lane - a.b0] = rel;
@@ -446,12 +450,12 @@ __global__ __launch_bounds__(256, P2PG_GROUPED_WAVES) void k_gossip_fused_groupe
   }
 }
 
-template <bool CH, int KT, bool PO = false>
+template <bool CH, int KT, bool PO = false, bool PL = false>
 hipError_t launch_lw(int lw, const DevGraph& g, const DevState& st, const RoundParams& p, hipStream_t s) {
   const int64_t ntasks = (g.V + 31) >> 5;
 #define P2PG_GROUPED(LWV)                                                                    \
-  hipLaunchKernelGGL((k_gossip_fused_grouped<CH, KT, LWV, PO>),                            \
-                     dim3(balanced_grid(k_gossip_fused_grouped<CH, KT, LWV, PO>, ntasks)), dim3(256), \
+  hipLaunchKernelGGL((k_gossip_fused_grouped<CH, KT, LWV, PO, PL>),                        \
+                     dim3(balanced_grid(k_gossip_fused_grouped<CH, KT, LWV, PO, PL>, ntasks)), dim3(256), \
                      0, s, g, st, p)
   switch (lw) {
     case 0: P2PG_GROUPED(0); break;
@@ -486,6 +490,16 @@ hipError_t launch_gossip_push_grouped(const DevGraph& g, const DevState& st, con
   if (p.fanout == 3)
     return ch ? launch_lw<true, 3, true>(lw, g, st, p, s) : launch_lw<false, 3, true>(lw, g, st, p, s);
   return ch ? launch_lw<true, 0, true>(lw, g, st, p, s) : launch_lw<false, 0, true>(lw, g, st, p, s);
+}
+
+hipError_t launch_gossip_pull_grouped(const DevGraph& g, const DevState& st, const RoundParams& p,
+                                      hipStream_t s) {
+  if (st.W > GROUPED_W_MAX || st.W < 1) return hipErrorInvalidValue;
+  int lw = 0;
+  while ((1 << lw) < st.W) ++lw;
+  // (no picks: the fanout template argument is irrelevant)
+  return p.churn_thr != 0 ? launch_lw<true, 0, false, true>(lw, g, st, p, s)
+                          : launch_lw<false, 0, false, true>(lw, g, st, p, s);
 }
 
 }  // namespace p2pg

@@ -195,8 +195,7 @@ struct FusedStage {
   int32_t u;        // the target peer
   uint32_t beg, end;
   uint64_t s;
-  int32_t v;
-  uint32_t r;
+  int32_t v;        // (the E row of slot j is row j itself: no per-lane row id is kept)
   bool act;
   uint32_t aword;
   uint64_t mr;
@@ -1379,7 +1378,6 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
   auto issue = [&](FusedStage& q) {
     q.act = false;
     q.v = 0;
-    q.r = 0;
     q.rv = 0;
     q.s = 0;
     q.u = next_peer(q.beg, q.end);
@@ -1389,7 +1387,6 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
     const uint32_t j = q.beg + lane;
     if (j < q.end) {
       q.v = ld_once(&g.colidx[j]);
-      q.r = (uint32_t)j;
       q.rv = ld_once(&g.rev[j]);
     }
   };
@@ -1425,7 +1422,7 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
       if (m) {
         const int idx = __builtin_ctzll(m);
         m &= m - 1ull;
-        sv[k] = (uint32_t)__builtin_amdgcn_readlane((int)q.r, idx);
+        sv[k] = q.beg + (uint32_t)idx;  // receiver-major E: the row of slot j is j
         am[k] = (uint64_t)readlane64((int64_t)q.am, idx);
       }
     }
@@ -1510,7 +1507,6 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
     PROF_MARK(0);
     {
       uint64_t m = a.mr;  // the rest of the first 64 slots, then further 64-slot chunks
-      uint32_t srow = a.r;
       uint64_t sam = a.am;
       uint32_t cb = a.beg;
       for (;;) {
@@ -1525,7 +1521,7 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
             if (m) {
               const int idx = __builtin_ctzll(m);
               m &= m - 1ull;
-              sv[k] = (uint32_t)__builtin_amdgcn_readlane((int)srow, idx);
+              sv[k] = cb + (uint32_t)idx;  // the E row of slot cb + idx (receiver-major)
               am[k] = (uint64_t)readlane64((int64_t)sam, idx);
             } else {
               sv[k] = 0u;
@@ -1542,11 +1538,9 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
         if (cb >= a.end) break;
         const uint32_t j = cb + lane;  // further chunks of a wide row: serial
         bool act = false;
-        srow = 0;
         sam = 0;
         if (j < a.end) {
           const int32_t v = g.colidx[j];
-          srow = (uint32_t)j;
           act = bit_test(Ap, v);
           if (act) sam = AWp[v];
         }
@@ -1944,8 +1938,30 @@ hipError_t launch_flood_pull(const DevGraph& g, const DevState& st, const RoundP
                      : pull_with_hubs<false, false>(g, st, p, hp, s);
 }
 
+static bool grouped_enabled();
+static bool grouped_pull_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("P2PG_GROUPED_PULL");
+    return !(e && std::strcmp(e, "0") == 0);
+  }();
+  return on;
+}
+
 hipError_t launch_gossip_pull(const DevGraph& g, const DevState& st, const RoundParams& p,
                               const HubPlan& hp, hipStream_t s) {
+  // narrow rows: several peers per wave (the grouped fused kernel without its pushes); the hubs
+  // are left to the hub items as in the fused rounds
+  if (grouped_enabled() && grouped_pull_enabled() && st.W <= GROUPED_W_MAX && p.phase < 0) {
+    if (hp.n_items)
+      hipLaunchKernelGGL((k_pull_hub_partial<false, true>), dim3(grid_tasks(hp.n_items)),
+                         dim3(256), 0, s, g, st, p, hp);
+    hipError_t r = launch_gossip_pull_grouped(g, st, p, s);
+    if (r != hipSuccess) return r;
+    if (hp.n_hubs)
+      hipLaunchKernelGGL((k_pull_hub_finalize<true>), dim3(grid_tasks(hp.n_hubs)), dim3(256), 0,
+                         s, g, st, p, hp);
+    return hipGetLastError();
+  }
   return pull_with_hubs<false, true>(g, st, p, hp, s);
 }
 
