@@ -1993,7 +1993,10 @@ hipError_t launch_gossip_update(const DevGraph& g, const DevState& st, const Rou
     const char* e = std::getenv("P2PG_UPDATE_G");
     return !(e && std::strcmp(e, "0") == 0);
   }();
-  if (narrow && st.W <= 32) {
+  // several touched peers per wave up to W = 16; at W = 32 (two per wave) the pipelined
+  // one-peer kernel is faster (c4 --msgs 2048, profiles/r03/ab_update_g.txt: 20.4 vs 19.65 ms;
+  // W = 16: 10.25 vs 13.95 ms, W = 8: 6.75 vs 12.1 ms)
+  if (narrow && st.W <= 16) {
     int lw = 0;
     while ((1 << lw) < st.W) ++lw;
     switch (lw) {
