@@ -1307,7 +1307,12 @@ constexpr int FG = P2PG_FG;
 #ifndef P2PG_FUSED_WAVES
 #define P2PG_FUSED_WAVES 4  // = 128 VGPRs: 4 waves per SIMD (the gathers spill a few registers per task, not per peer)
 #endif
-template <bool CHURN, int K>
+// PO (push only): the first dense round after an update (16 < W <= 64, packed E) -- the peers are
+// the round's active non-hub peers, their arrivals are their own frontier rows F[r&1] (dedup,
+// counters, bitmaps and AW were done by the update), and only the picks and the E stores run,
+// through the same software pipeline (replaces k_gossip_scatter<.., true>: one wave per source
+// with a two-deep prefetch, ~7.3 ms per c4 step at W = 64 and at W = 32).
+template <bool CHURN, int K, bool PO = false>
 __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph g, DevState st,
                                                                         RoundParams p) {
   __shared__ ScatterLds lds[WPB];
@@ -1340,7 +1345,7 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
   auto prefetch = [&](int64_t t) {
     pf_task = t;
     if (t < 0) return;
-    pf_s = st.S[t];
+    pf_s = PO ? st.A[cur][t] : st.S[t];  // PO: the active peers; else the saturated ones
     pf_h = g.H ? g.H[t] : 0u;
     const int64_t u0 = t << 5;
     pf_rp = (lane <= 32 && u0 + lane <= V) ? (uint32_t)g.rowptr[u0 + lane] : 0u;
@@ -1356,13 +1361,13 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
       const int64_t t = pf_task;
       if (t < 0) return -1;
       const int64_t u0 = t << 5;
-      uint32_t todo = ~(uint32_t)__builtin_amdgcn_readfirstlane((int)pf_s) &
-                      ~(uint32_t)__builtin_amdgcn_readfirstlane((int)pf_h);
+      const uint32_t sw = (uint32_t)__builtin_amdgcn_readfirstlane((int)pf_s);
+      uint32_t todo = (PO ? sw : ~sw) & ~(uint32_t)__builtin_amdgcn_readfirstlane((int)pf_h);
       if (V - u0 < 32) todo &= (1u << (V - u0)) - 1u;
       rp = pf_rp;
       prefetch(t + tstride < ntasks ? t + tstride : -1);
       if (!todo) {
-        if (lane == 0) st.A[cur][t] = 0u;
+        if (!PO && lane == 0) st.A[cur][t] = 0u;
         continue;
       }
       it_u0 = (int32_t)u0;
@@ -1383,16 +1388,17 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
     q.u = next_peer(q.beg, q.end);
     q.b = q.u < 0 ? -1 : 0;
     if (q.u < 0) return;
-    if (valid) q.s = ld_once(&st.seen[(int64_t)q.u * W + lane]);
+    // PO: the peer's frontier row (its new receipts of this round) instead of its seen row
+    if (valid) q.s = ld_once(&(PO ? Fc : st.seen)[(int64_t)q.u * W + lane]);
     const uint32_t j = q.beg + lane;
     if (j < q.end) {
-      q.v = ld_once(&g.colidx[j]);
+      if (!PO) q.v = ld_once(&g.colidx[j]);
       q.rv = ld_once(&g.rev[j]);
     }
   };
   // loads only; gather() tests the bit (see k_pull1)
   auto activity = [&](FusedStage& q) {
-    if (q.b < 0) return;
+    if (PO || q.b < 0) return;
     const uint32_t j = q.beg + lane;
     q.am = 0;
     q.aword = 0;
@@ -1406,6 +1412,12 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
   // first 64) still to gather
   uint64_t X[FG];
   auto gather = [&](const FusedStage& q, uint64_t& mr) {
+    if (PO) {  // no arrivals to gather: the frontier row came with the row stage
+#pragma unroll
+      for (int k = 0; k < FG; ++k) X[k] = 0ull;
+      mr = 0;
+      return;
+    }
     const uint64_t needm = __ballot((fm & ~q.s) != 0ull);
     const uint32_t jq = q.beg + lane;
     uint64_t m = __ballot(jq < q.end && ((q.aword >> (q.v & 31)) & 1u));
@@ -1439,7 +1451,7 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
   uint32_t aw = 0, nsat = 0;
   auto finish_task = [&]() {
     if (ct < 0) return;
-    if (lane == 0) {
+    if (!PO && lane == 0) {  // PO: the update wrote the task's bitmaps
       st.A[cur][ct] = aw;
       if (nsat) atomicOr(&st.S[ct], nsat);  // this wave owns the task: no other writer
     }
@@ -1499,13 +1511,13 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
       ct = u >> 5;
     }
     const uint64_t deg = (uint64_t)(a.end - a.beg);
-    const uint64_t need = fm & ~a.s;
+    const uint64_t need = PO ? ~0ull : fm & ~a.s;
     const uint64_t needm = __ballot(need != 0ull);
     uint64_t acc = 0;
 #pragma unroll
     for (int k = 0; k < FG; ++k) acc |= X[k];
     PROF_MARK(0);
-    {
+    if (!PO) {
       uint64_t m = a.mr;  // the rest of the first 64 slots, then further 64-slot chunks
       uint64_t sam = a.am;
       uint32_t cb = a.beg;
@@ -1561,9 +1573,9 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
     activity(cc);
     issue(d);
     PROF_MARK(2);
-    const uint64_t nw = acc & need;
+    const uint64_t nw = PO ? a.s : acc & need;
     const uint64_t wm = __ballot(nw != 0ull);
-    if (nw) {
+    if (!PO && nw) {
       st_frow(&st.seen[u * W + lane], a.s | nw);
       const uint32_t pc = (uint32_t)__popcll(nw);
       const uint32_t per_bit = deg < (uint64_t)p.fanout ? (uint32_t)deg : (uint32_t)p.fanout;
@@ -1573,12 +1585,14 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
       c[ST_WEDGES] += (uint32_t)deg;
     }
     if (wm) {
-      if (valid && p.store_f) st_frow(&Fc[u * W + lane], nw);
-      aw |= 1u << (u & 31);
-      if (lane == 0) {
-        st.AW[cur][u] = wm;
-        c[ST_ACTIVE_W] += 1u << 16;  // ST_ACTIVE_V, packed (see finish_task)
-        c[ST_DEG_ACT] += (uint32_t)deg;
+      if (!PO) {
+        if (valid && p.store_f) st_frow(&Fc[u * W + lane], nw);
+        aw |= 1u << (u & 31);
+        if (lane == 0) {
+          st.AW[cur][u] = wm;
+          c[ST_ACTIVE_W] += 1u << 16;  // ST_ACTIVE_V, packed (see finish_task)
+          c[ST_DEG_ACT] += (uint32_t)deg;
+        }
       }
       // this round's pushes, GCHUNK connections at a time.  a.rv holds the receiver slots of
       // the first 64 (arrived: see the explicit wait above); wider rows load the next 64
@@ -1610,7 +1624,7 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
       }
     }
     PROF_MARK(3);
-    if (!__ballot(valid && (a.s | nw) != fm)) nsat |= 1u << (u & 31);
+    if (!PO && !__ballot(valid && (a.s | nw) != fm)) nsat |= 1u << (u & 31);
   };
   for (;;) {
     if (sA.b < 0) break;
@@ -2053,6 +2067,30 @@ hipError_t launch_gossip_scatter(const DevGraph& g, const DevState& st, const Ro
   if (store_e && push_grouped && grouped_enabled() && st.W <= GROUPED_W_MAX &&
       (n_big == 0 || (big_items && wide_big))) {
     hipError_t r = launch_gossip_push_grouped(g, st, p, s);
+    if (r != hipSuccess) return r;
+    return launch_wide_push_e(g, st, p, big_items, n_big, wide_big, n_wide_big, s);
+  }
+  // wider packed rows: the push-only mode of the one-peer-per-wave fused kernel, hubs by atomics
+  static const bool push_fused = [] {  // P2PG_PUSH_FUSED=0: one wave per source (A/B)
+    const char* e = std::getenv("P2PG_PUSH_FUSED");
+    return !(e && std::strcmp(e, "0") == 0);
+  }();
+  if (store_e && push_fused && st.W <= 64 && st.AW[p.round & 1] != nullptr &&
+      (n_big == 0 || (big_items && wide_big))) {
+#define P2PG_FUSED_PO(CH, KK)                                                                       \
+  hipLaunchKernelGGL((k_gossip_fused<CH, KK, true>),                                              \
+                     dim3(balanced_grid(k_gossip_fused<CH, KK, true>, (g.V + 31) >> 5)), dim3(256), \
+                     0, s, g, st, p)
+    const bool ch = p.churn_thr != 0;
+    switch (p.fanout) {
+      case 1: if (ch) P2PG_FUSED_PO(true, 1); else P2PG_FUSED_PO(false, 1); break;
+      case 2: if (ch) P2PG_FUSED_PO(true, 2); else P2PG_FUSED_PO(false, 2); break;
+      case 3: if (ch) P2PG_FUSED_PO(true, 3); else P2PG_FUSED_PO(false, 3); break;
+      case 4: if (ch) P2PG_FUSED_PO(true, 4); else P2PG_FUSED_PO(false, 4); break;
+      default: if (ch) P2PG_FUSED_PO(true, 0); else P2PG_FUSED_PO(false, 0); break;
+    }
+#undef P2PG_FUSED_PO
+    hipError_t r = hipGetLastError();
     if (r != hipSuccess) return r;
     return launch_wide_push_e(g, st, p, big_items, n_big, wide_big, n_wide_big, s);
   }
