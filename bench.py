@@ -50,7 +50,8 @@ GOSSIP_SEED, CHURN_SEED = 0x5EED, 0xC0FFEE
 
 KCLASS = ("seed", "flood_pull", "gossip_scatter_atomic", "record", "gossip_update", "gossip_pull",
           "gossip_scatter_store", "gossip_fused")
-ATOMIC, EDGE, FUSED = 1, 2, 3  # p2pg_round_stats.push_form (include/p2pgpu.h P2PG_PUSH_*)
+ATOMIC, EDGE, FUSED, UPDATE_EDGE = 1, 2, 3, 4  # p2pg_round_stats.push_form (P2PG_PUSH_*)
+E_FORMS = (EDGE, FUSED, UPDATE_EDGE)  # pushes into the E plane: the next round pulls them
 
 
 def push_forms(rounds):
@@ -86,6 +87,8 @@ def model_bytes(rounds, mode, W, packed=None):
     fused round r (pull + pushes in one pass, gossip_fused):
                                         8*wedges[r-1] + 24*words[r] + 4*degact[r] + 8*wedges[r]
                                         (the frontier row is not re-read: no 8*words[r])
+    update + edge pushes in one pass (UPDATE_EDGE, timed with gossip_scatter_store): the update's
+                                        and the edge pushes' bytes, both in that class
     """
     b = {k: 0 for k in KCLASS}
     if packed is None:
@@ -107,12 +110,13 @@ def model_bytes(rounds, mode, W, packed=None):
                                   + e_bytes(r))
             continue
         if i >= 1:
-            if forms[i - 1] in (EDGE, FUSED):
+            if forms[i - 1] in E_FORMS:
                 b["gossip_pull"] += e_bytes(rounds[i - 1]) + 24 * r.active_words
             else:
-                b["gossip_update"] += 24 * r.touched_words + 16 * r.active_words
+                upd = "gossip_scatter_store" if forms[i] == UPDATE_EDGE else "gossip_update"
+                b[upd] += 24 * r.touched_words + 16 * r.active_words
         common = 8 * r.active_words + 8 * r.active_vertices + 4 * r.deg_active
-        if forms[i] == EDGE:
+        if forms[i] in (EDGE, UPDATE_EDGE):
             b["gossip_scatter_store"] += common + e_bytes(r)
         else:
             b["gossip_scatter_atomic"] += common + 16 * r.scatter_words
@@ -140,7 +144,8 @@ def survey_bytes_kernel(rounds, mode, kclass):
     tot = 0
     for i in range(1, len(rounds)):
         consumer = ("gossip_fused" if forms[i] == FUSED else
-                    "gossip_pull" if forms[i - 1] in (EDGE, FUSED) else "gossip_update")
+                    "gossip_pull" if forms[i - 1] in E_FORMS else
+                    "gossip_scatter_store" if forms[i] == UPDATE_EDGE else "gossip_update")
         if consumer != kclass:
             continue
         p, r = rounds[i - 1], rounds[i]

@@ -50,6 +50,8 @@ extern "C" {
 #define P2PG_PUSH_ATOMIC 1 /* gossip sparse round: row atomicOr into the targets' rows    */
 #define P2PG_PUSH_EDGE 2   /* gossip dense round: per-connection mask stores (E plane)    */
 #define P2PG_PUSH_FUSED 3  /* as EDGE, in one pass with this round's pull of E            */
+#define P2PG_PUSH_UPDATE_EDGE 4 /* as EDGE, in one pass with this round's update (the    */
+                                /* row pushes of a sparse round before it)                */
 
 #define P2PG_FLAG_RECORD 1u /* keep hop/parent planes [V][M] (validation scale)            */
 #define P2PG_FLAG_TIMING 2u /* per-kernel HIP-event timing (p2pg_kernel_times)              */

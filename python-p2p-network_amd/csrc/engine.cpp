@@ -90,6 +90,11 @@ struct p2pg_engine {
   bool frontier_kept_prev = true;  // ... and F[round&1] the round before (delivery parents)
   uint64_t prev_aw = 0, prev_av = 0;  // active words / rows of the previous round
   uint64_t last_new = 0;       // first receipts of the last round run
+  uint64_t prev2_aw = 0, prev2_av = 0, prev2_new = 0;  // the same, one round earlier
+  int update_push = -1;        // the first dense round after a sparse one: its update and its
+                               // E pushes in one pass (launch_gossip_update_push) -- -1 when the
+                               // round is predicted dense (predict_dense), 0 never, 1 whenever
+                               // the rows allow it (P2PG_UPDATE_PUSH)
   int32_t* d_src = nullptr;
   DevState st{};
   size_t plane_bytes = 0, bm_bytes = 0;
@@ -359,6 +364,31 @@ bool wide_atomic_on(const p2pg_engine* e) {
   return e->wide_atomic && e->W <= 64 && (e->W <= PACK_W_MAX_PLAIN || e->st.AW[0]);
 }
 
+// Will the pushes of round e->round (a round after a sparse one, before its update ran) be dense
+// by the rule the engine applies to its own stats (use_e below)?  Rising phase only: active words
+// grow by the last round's factor and inactive peers shrink by it, with a 15 % margin on the word
+// test.  On config 4's recorded rounds at 512 / 1024 / 2048 / 4096 broadcasts this names exactly
+// the first dense round at W = 32 / 64 and none at W <= 16 (no false positive).  A wrong guess
+// changes the push form of one round, never a result.
+bool predict_dense(const p2pg_engine* e) {
+  if (e->prev2_aw == 0 || e->prev2_av == 0 || e->last_new <= e->prev2_new) return false;
+  const double V = (double)e->V;
+  const double in1 = V - (double)e->prev_av, in2 = V - (double)e->prev2_av;
+  if (in2 <= 0.0) return false;
+  const double est_av = V - in1 * (in1 / in2);
+  const double est_aw = (double)e->prev_aw * ((double)e->prev_aw / (double)e->prev2_aw);
+  return est_av > 0.0 && est_aw >= 1.15 * e->e_thresh * est_av * (double)e->W &&
+         est_av >= e->v_thresh * V;
+}
+
+// Run this round's update and its (dense) pushes in one pass?
+bool update_push_round(const p2pg_engine* e, const RoundParams& p) {
+  if (e->update_push == 0 || e->cfg.mode != P2PG_MODE_GOSSIP || e->push_mode != 0 || e->d_gid ||
+      p.phase >= 0 || !e->st.E[0] || !wide_atomic_on(e) || !gossip_update_push_supported(e->st))
+    return false;
+  return e->update_push == 1 || predict_dense(e);
+}
+
 // After the stream synced on a round whose push ran lane-parallel: the list must have held
 // every (peer, word) pair (n_words is the frontier's own count, so a shortfall is a bug).
 int check_scatter_list(p2pg_engine* e, unsigned long long listed) {
@@ -478,6 +508,7 @@ int p2pg_create(const p2pg_config* cfg, p2pg_engine** out) {
   if (const char* f = std::getenv("P2PG_SPARSE_LP")) e->sparse_lp = std::strcmp(f, "0") != 0;
   if (const char* f = std::getenv("P2PG_PUSH_DEDUP")) e->push_dedup = std::atoi(f);
   if (const char* f = std::getenv("P2PG_WIDE_ATOMIC")) e->wide_atomic = std::strcmp(f, "0") != 0;
+  if (const char* f = std::getenv("P2PG_UPDATE_PUSH")) e->update_push = std::atoi(f);
   if (const char* m = std::getenv("P2PG_GOSSIP_PUSH"))
     e->push_mode = !std::strcmp(m, "atomic") ? 1 : (!std::strcmp(m, "store") ? 2 : 0);
   HIPCHK(e, hipSetDevice(cfg->device));
@@ -688,6 +719,7 @@ int p2pg_reset(p2pg_engine* e) {
   free_arr(e);
   e->prev_aw = e->prev_av = 0;
   e->last_new = 0;
+  e->prev2_aw = e->prev2_av = e->prev2_new = 0;
   for (int i = 0; i < P2PG_KCLASS_N; ++i) {
     e->kms[i] = 0;
     e->klaunch[i] = 0;
@@ -752,7 +784,7 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
   }
   e->begun = false;
   const bool gossip = e->cfg.mode == P2PG_MODE_GOSSIP;
-  bool fused_round = false;
+  bool fused_round = false, up_round = false;
   uint64_t host_new = 0, host_relays = 0, host_av = 0, host_aw = 0, host_wedge = 0, host_degact = 0;
   if (e->round == 0) {
     if ((rc = timed(e, 0, [&] { return launch_zero_rows(s.F[0], e->W, e->d_src, e->M, e->stream); }))) return rc;
@@ -811,6 +843,16 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
     } else {
       if ((rc = timed(e, 5, [&] { return launch_gossip_pull(g, s, p, e->hp, e->stream); }))) return rc;
     }
+  } else if (update_push_round(e, p)) {
+    // the first dense round after a sparse one: update and E pushes in one pass (timed with the
+    // store pushes); the frontier rows follow the fused rounds' rule
+    up_round = true;
+    p.store_f = (e->skip_frontier && !s.hop) ? 0 : 1;
+    if ((rc = timed(e, 6, [&] {
+           return launch_gossip_update_push(g, s, p, e->d_hub_big, e->n_hub_big, e->d_wide_big,
+                                            e->n_wide_big, e->stream);
+         })))
+      return rc;
   } else {
     if ((rc = timed(e, 4, [&] { return launch_gossip_update(g, s, p, e->stream); }))) return rc;
   }
@@ -838,7 +880,7 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
     }
     return P2PG_OK;
   };
-  if (gossip && fused_round) {
+  if (gossip && (fused_round || up_round)) {
     e->last_push_e = true;  // the fused launches pushed every source of this round
   } else if (gossip) {
     // push form for this round's sends: row atomics when the frontier is sparse, whole-row
@@ -885,7 +927,7 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
 #endif
   const bool active = tot[ST_NEW] != 0;
   e->frontier_kept_prev = e->frontier_kept;
-  e->frontier_kept = !(fused_round && !p.store_f && active);
+  e->frontier_kept = !((fused_round || up_round) && !p.store_f && active);
   if (out) {
     out->round = e->round;
     out->active = active ? 1 : 0;
@@ -899,9 +941,13 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
     out->touched_words = tot[ST_AUX];
     out->push_form = !gossip ? P2PG_PUSH_NONE
                      : fused_round ? P2PG_PUSH_FUSED
+                     : up_round ? P2PG_PUSH_UPDATE_EDGE
                      : e->last_push_e ? P2PG_PUSH_EDGE : P2PG_PUSH_ATOMIC;
   }
   e->total_relays += tot[ST_RELAYS];
+  e->prev2_aw = e->prev_aw;
+  e->prev2_av = e->prev_av;
+  e->prev2_new = e->last_new;
   e->prev_aw = tot[ST_ACTIVE_W];
   e->prev_av = tot[ST_ACTIVE_V];
   e->last_new = tot[ST_NEW];
@@ -1492,6 +1538,7 @@ int p2pg_restore(p2pg_engine* e, const void* buf, int64_t size) {
   e->total_relays = h.total_relays;
   e->prev_aw = h.prev_aw;
   e->prev_av = h.prev_av;
+  e->prev2_aw = e->prev2_av = e->prev2_new = 0;  // no growth history: no update+push prediction
   const char* in = (const char*)buf;
   size_t off = sizeof(h);
   rc = for_planes(e, with_next, [&](void* dev, size_t n) -> int {

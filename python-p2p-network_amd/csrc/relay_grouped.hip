@@ -494,7 +494,7 @@ hipError_t launch_gossip_push_grouped(const DevGraph& g, const DevState& st, con
 
 hipError_t launch_gossip_pull_grouped(const DevGraph& g, const DevState& st, const RoundParams& p,
                                       hipStream_t s) {
-  if (st.W > GROUPED_W_MAX || st.W < 1) return hipErrorInvalidValue;
+  if (st.W > GROUPED_PULL_W_MAX || st.W < 1) return hipErrorInvalidValue;
   int lw = 0;
   while ((1 << lw) < st.W) ++lw;
   // (no picks: the fanout template argument is irrelevant)

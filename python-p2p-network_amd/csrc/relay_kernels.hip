@@ -1307,14 +1307,20 @@ constexpr int FG = P2PG_FG;
 #ifndef P2PG_FUSED_WAVES
 #define P2PG_FUSED_WAVES 4  // = 128 VGPRs: 4 waves per SIMD (the gathers spill a few registers per task, not per peer)
 #endif
-// PO (push only): the first dense round after an update (16 < W <= 64, packed E) -- the peers are
-// the round's active non-hub peers, their arrivals are their own frontier rows F[r&1] (dedup,
-// counters, bitmaps and AW were done by the update), and only the picks and the E stores run,
-// through the same software pipeline (replaces k_gossip_scatter<.., true>: one wave per source
-// with a two-deep prefetch, ~7.3 ms per c4 step at W = 64 and at W = 32).
-template <bool CHURN, int K, bool PO = false>
+// MODE 0: the fused dense round above.
+// MODE 1, PO (push only): the first dense round after an update (16 < W <= 64, packed E) -- the
+// peers are the round's active non-hub peers, their arrivals are their own frontier rows F[r&1]
+// (dedup, counters, bitmaps and AW were done by the update), and only the picks and the E stores
+// run, through the same software pipeline (replaces k_gossip_scatter<.., true>: one wave per
+// source with a two-deep prefetch, ~7.3 ms per c4 step at W = 64 and at W = 32).
+// MODE 2, UP (update + push): the same first dense round with the update folded in -- the peers
+// are the touched non-hub peers (T[r&1]), their arrivals the row pushes next[r&1] of the sparse
+// round before (read and cleared), then dedup, frontier row, bitmaps, counters and the pushes as
+// in a fused round; the touched hubs are left in T for a hub-only update (launch_gossip_update_push).
+template <bool CHURN, int K, int MODE = 0>
 __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph g, DevState st,
                                                                         RoundParams p) {
+  constexpr bool PO = MODE == 1, UP = MODE == 2;
   __shared__ ScatterLds lds[WPB];
   const int lane = threadIdx.x & 63;
   const int wib = wave_in_block();
@@ -1345,7 +1351,8 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
   auto prefetch = [&](int64_t t) {
     pf_task = t;
     if (t < 0) return;
-    pf_s = PO ? st.A[cur][t] : st.S[t];  // PO: the active peers; else the saturated ones
+    // PO: the active peers; UP: the touched ones; else the saturated ones
+    pf_s = PO ? st.A[cur][t] : UP ? st.T[cur][t] : st.S[t];
     pf_h = g.H ? g.H[t] : 0u;
     const int64_t u0 = t << 5;
     pf_rp = (lane <= 32 && u0 + lane <= V) ? (uint32_t)g.rowptr[u0 + lane] : 0u;
@@ -1362,8 +1369,11 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
       if (t < 0) return -1;
       const int64_t u0 = t << 5;
       const uint32_t sw = (uint32_t)__builtin_amdgcn_readfirstlane((int)pf_s);
-      uint32_t todo = (PO ? sw : ~sw) & ~(uint32_t)__builtin_amdgcn_readfirstlane((int)pf_h);
+      const uint32_t hw = (uint32_t)__builtin_amdgcn_readfirstlane((int)pf_h);
+      uint32_t todo = (PO || UP ? sw : ~sw) & ~hw;
       if (V - u0 < 32) todo &= (1u << (V - u0)) - 1u;
+      // UP: the non-hub touched peers are consumed here (only this wave reads this T word)
+      if (UP && lane == 0 && (sw & ~hw)) st.T[cur][t] = sw & hw;
       rp = pf_rp;
       prefetch(t + tstride < ntasks ? t + tstride : -1);
       if (!todo) {
@@ -1388,17 +1398,19 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
     q.u = next_peer(q.beg, q.end);
     q.b = q.u < 0 ? -1 : 0;
     if (q.u < 0) return;
-    // PO: the peer's frontier row (its new receipts of this round) instead of its seen row
+    // PO: the peer's frontier row (its new receipts of this round) instead of its seen row;
+    // UP: the seen row and, in the stage's mask field, the push row (the arrivals)
     if (valid) q.s = ld_once(&(PO ? Fc : st.seen)[(int64_t)q.u * W + lane]);
+    if (UP) q.am = valid ? st.next[cur][(int64_t)q.u * W + lane] : 0ull;
     const uint32_t j = q.beg + lane;
     if (j < q.end) {
-      if (!PO) q.v = ld_once(&g.colidx[j]);
+      if (MODE == 0) q.v = ld_once(&g.colidx[j]);
       q.rv = ld_once(&g.rev[j]);
     }
   };
   // loads only; gather() tests the bit (see k_pull1)
   auto activity = [&](FusedStage& q) {
-    if (PO || q.b < 0) return;
+    if (MODE != 0 || q.b < 0) return;
     const uint32_t j = q.beg + lane;
     q.am = 0;
     q.aword = 0;
@@ -1412,7 +1424,7 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
   // first 64) still to gather
   uint64_t X[FG];
   auto gather = [&](const FusedStage& q, uint64_t& mr) {
-    if (PO) {  // no arrivals to gather: the frontier row came with the row stage
+    if (MODE != 0) {  // no arrivals to gather: they came with the row stage
 #pragma unroll
       for (int k = 0; k < FG; ++k) X[k] = 0ull;
       mr = 0;
@@ -1516,8 +1528,9 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
     uint64_t acc = 0;
 #pragma unroll
     for (int k = 0; k < FG; ++k) acc |= X[k];
+    if (UP) acc = a.am;  // the push row
     PROF_MARK(0);
-    if (!PO) {
+    if (MODE == 0) {
       uint64_t m = a.mr;  // the rest of the first 64 slots, then further 64-slot chunks
       uint64_t sam = a.am;
       uint32_t cb = a.beg;
@@ -1566,6 +1579,10 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
     // wait would stall until those gathers return).
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     PROF_MARK(1);
+    if (UP && acc) {  // the push row is consumed: all-zero again outside touched rows
+      st_prow(&st.next[cur][(int64_t)u * W + lane], 0ull);
+      c[ST_AUX] += 1;  // touched (pushed-to) words consumed
+    }
     flush_pending();
     // advance the pipeline before this target's stores and picks: gathers of t+1 (their
     // activity words were loaded a target ago), activity words of t+2, rows of t+3
@@ -1965,7 +1982,7 @@ hipError_t launch_gossip_pull(const DevGraph& g, const DevState& st, const Round
                               const HubPlan& hp, hipStream_t s) {
   // narrow rows: several peers per wave (the grouped fused kernel without its pushes); the hubs
   // are left to the hub items as in the fused rounds
-  if (grouped_enabled() && grouped_pull_enabled() && st.W <= GROUPED_W_MAX && p.phase < 0) {
+  if (grouped_enabled() && grouped_pull_enabled() && st.W <= GROUPED_PULL_W_MAX && p.phase < 0) {
     if (hp.n_items)
       hipLaunchKernelGGL((k_pull_hub_partial<false, true>), dim3(grid_tasks(hp.n_items)),
                          dim3(256), 0, s, g, st, p, hp);
@@ -2078,8 +2095,8 @@ hipError_t launch_gossip_scatter(const DevGraph& g, const DevState& st, const Ro
   if (store_e && push_fused && st.W <= 64 && st.AW[p.round & 1] != nullptr &&
       (n_big == 0 || (big_items && wide_big))) {
 #define P2PG_FUSED_PO(CH, KK)                                                                       \
-  hipLaunchKernelGGL((k_gossip_fused<CH, KK, true>),                                              \
-                     dim3(balanced_grid(k_gossip_fused<CH, KK, true>, (g.V + 31) >> 5)), dim3(256), \
+  hipLaunchKernelGGL((k_gossip_fused<CH, KK, 1>),                                                 \
+                     dim3(balanced_grid(k_gossip_fused<CH, KK, 1>, (g.V + 31) >> 5)), dim3(256),    \
                      0, s, g, st, p)
     const bool ch = p.churn_thr != 0;
     switch (p.fanout) {
@@ -2110,6 +2127,46 @@ static bool grouped_enabled() {
     return !(e && std::strcmp(e, "0") == 0);
   }();
   return on;
+}
+
+bool gossip_update_push_supported(const DevState& st) {
+  return st.W > 16 && st.W <= 64 && st.AW[0] != nullptr && st.E[0] != nullptr &&
+         !(grouped_enabled() && st.W <= GROUPED_W_MAX);
+}
+
+hipError_t launch_gossip_update_push(const DevGraph& g, const DevState& st, const RoundParams& p,
+                                     const int64_t* big_items, int64_t n_big,
+                                     const int32_t* wide_big, int64_t n_wide_big, hipStream_t s) {
+  if (!gossip_update_push_supported(st) || p.phase >= 0 || (n_big && !(big_items && wide_big)) ||
+      (n_wide_big && !g.H))
+    return hipErrorInvalidValue;
+#define P2PG_FUSED_UP(CH, KK)                                                                       \
+  hipLaunchKernelGGL((k_gossip_fused<CH, KK, 2>),                                                 \
+                     dim3(balanced_grid(k_gossip_fused<CH, KK, 2>, (g.V + 31) >> 5)), dim3(256),    \
+                     0, s, g, st, p)
+  const bool ch = p.churn_thr != 0;
+  switch (p.fanout) {
+    case 1: if (ch) P2PG_FUSED_UP(true, 1); else P2PG_FUSED_UP(false, 1); break;
+    case 2: if (ch) P2PG_FUSED_UP(true, 2); else P2PG_FUSED_UP(false, 2); break;
+    case 3: if (ch) P2PG_FUSED_UP(true, 3); else P2PG_FUSED_UP(false, 3); break;
+    case 4: if (ch) P2PG_FUSED_UP(true, 4); else P2PG_FUSED_UP(false, 4); break;
+    default: if (ch) P2PG_FUSED_UP(true, 0); else P2PG_FUSED_UP(false, 0); break;
+  }
+#undef P2PG_FUSED_UP
+  hipError_t r = hipGetLastError();
+  if (r != hipSuccess) return r;
+  if (g.H) {
+    // the touched hubs (left in T): the update's second phase over the hub bitmap, which ORs
+    // their activity bits into the words the fused pass wrote
+    RoundParams ph = p;
+    ph.border = g.H;
+    ph.phase = 1;
+    const int grid = (int)std::min<int64_t>(grid_tasks((g.V + 31) >> 5), 1024);
+    hipLaunchKernelGGL(k_gossip_update1, dim3(grid), dim3(256), 0, s, g, st, ph);
+    r = hipGetLastError();
+    if (r != hipSuccess) return r;
+  }
+  return launch_wide_push_e(g, st, p, big_items, n_big, wide_big, n_wide_big, s);
 }
 
 bool gossip_fused_supported(const DevState& st) {

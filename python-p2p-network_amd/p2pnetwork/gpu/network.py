@@ -27,7 +27,7 @@ from . import _lib
 from .graph import PeerGraph
 
 # p2pg_round_stats.push_form (include/p2pgpu.h P2PG_PUSH_*)
-PUSH_FORMS = ("none", "atomic", "edge", "fused")
+PUSH_FORMS = ("none", "atomic", "edge", "fused", "update_edge")
 
 STAT_FIELDS = ("round", "active", "new_deliveries", "relays", "active_vertices", "active_words",
                "wedges", "deg_active", "scatter_words", "touched_words")

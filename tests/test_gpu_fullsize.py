@@ -123,16 +123,19 @@ def _hub_graph(V, m, seed):
     return PeerGraph.from_edges(g.V, e)
 
 
-@pytest.mark.parametrize("push", ["auto", "store_unfused"])
+@pytest.mark.parametrize("push", ["auto", "store_unfused", "update_push"])
 @pytest.mark.parametrize("V,M,fanout,churn", [(200_000, 1500, 3, 0.1), (120_000, 2048, 4, 0.0)])
 def test_gossip_wide_rows_hubs_churn_match_c_oracle(V, M, fanout, churn, push, monkeypatch):
     """Rows of 24 and 32 words (W > 16: one peer per wave, packed E rows and slot words) with
     a ragged last word, churn (lost sends leave their slot word empty) and hubs: the whole
-    seen plane and every per-round counter == the C oracle, fused and unfused."""
+    seen plane and every per-round counter == the C oracle, fused and unfused, and with every
+    round after a sparse one run as update + E pushes in one pass (P2PG_UPDATE_PUSH=1: touched
+    hubs by the hub-only update and atomics)."""
     from p2pnetwork.gpu import GraphNetwork, make_sources
     from p2pnetwork.gpu.network import churn_threshold
     monkeypatch.setenv("P2PG_GOSSIP_PUSH", "auto")
     monkeypatch.setenv("P2PG_FUSED", "0" if push == "store_unfused" else "1")
+    monkeypatch.setenv("P2PG_UPDATE_PUSH", "1" if push == "update_push" else "0")
     monkeypatch.setenv("P2PG_V_THRESH", "0.3")  # dense rounds from 30 % active peers on
     g = _hub_graph(V, 4, seed=V + M)
     src = make_sources(g.V, M, seed=7)
@@ -143,7 +146,8 @@ def test_gossip_wide_rows_hubs_churn_match_c_oracle(V, M, fanout, churn, push, m
         rounds = net.run()
         seen = net.seen_plane()
     forms = {r.push_form for r in rounds if r.new_deliveries}
-    assert (3 if push == "auto" else 2) in forms, forms  # dense rounds ran
+    assert (2 if push == "store_unfused" else 3) in forms, forms  # dense rounds ran
+    assert (push == "update_push") == (4 in forms), forms
     ora = coracle.run(g.rowptr, g.colidx, src, "gossip", fanout, GSEED, churn_threshold=thr,
                       churn_seed=CSEED, record=False, want_seen=True)
     np.testing.assert_array_equal(seen, ora.seen)

@@ -312,7 +312,7 @@ def test_gpu_sparse_push_dedup_matches_golden(name, dedup, monkeypatch):
     assert_rounds_equal(rounds, ora.rounds)
 
 
-@pytest.mark.parametrize("push", ["atomic", "store", "store_unfused"])
+@pytest.mark.parametrize("push", ["atomic", "store", "store_unfused", "auto_update"])
 @pytest.mark.parametrize("kind,p,M,thr,fanout", [
     ("hub", dict(V=1500, m=3, star=1100), 64, 0, 3),
     ("hub", dict(V=1500, m=3, star=300), 256, 0, 3),
@@ -333,6 +333,9 @@ def test_gpu_gossip_push_forms_match_oracle(kind, p, M, thr, fanout, push, monke
     from p2pnetwork.gpu import make_sources
     monkeypatch.setenv("P2PG_GOSSIP_PUSH", push.split("_")[0])
     monkeypatch.setenv("P2PG_FUSED", "0" if push == "store_unfused" else "1")
+    # auto_update: every round after a sparse one runs its update and dense pushes in one pass
+    # where the rows allow it (16 < W <= 64)
+    monkeypatch.setenv("P2PG_UPDATE_PUSH", "1" if push == "auto_update" else "0")
     seed = zlib.crc32(repr((kind, M, thr, fanout)).encode()) & 0xFFFF
     g = make_graph(kind, p, seed)
     src = make_sources(g.V, M, seed=seed + 3)
@@ -341,7 +344,9 @@ def test_gpu_gossip_push_forms_match_oracle(kind, p, M, thr, fanout, push, monke
         rounds = net.run()
         hop, parent = net.hop_parent()
     forms = [r.push_form for r in rounds if r.new_deliveries]
-    if push == "store" and M <= 4096:
+    if push == "auto_update":
+        assert (4 in forms) == (1024 < M <= 4096), forms
+    elif push == "store" and M <= 4096:
         assert forms[0] == 2 and all(f == 3 for f in forms[1:]), forms
     elif push.startswith("store"):
         assert all(f == 2 for f in forms), forms
