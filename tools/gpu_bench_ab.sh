@@ -15,7 +15,7 @@ for rep in $(seq 1 $reps); do
       *) lib=python-p2p-network_amd/csrc/variants/$v/libp2pgpu.so ;;
     esac
     f=gpurun_out/$tag/m${msgs}_$(echo "$v" | tr ':=,' '___')_$rep.json
-    env P2PG_LIB=$lib $envs timeout -k 10 180 python bench.py --steps 5 --warmup 1 --msgs $msgs --no-cpu-baseline > $f 2> $f.err || { tail -20 $f.err; exit 1; }
+    env P2PG_LIB=$lib $envs timeout -k 10 180 python bench.py --workload ${AB_WORKLOAD:-c4} --steps ${AB_STEPS:-5} --warmup 1 --msgs $msgs --no-cpu-baseline > $f 2> $f.err || { tail -20 $f.err; exit 1; }
     python3 - "$f" "$v" <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
