@@ -54,7 +54,7 @@ def test_survey_bytes_formula_per_round():
     assert tot == want > 0
 
 
-@pytest.mark.parametrize("pattern", ["all_atomic", "dense_middle"])
+@pytest.mark.parametrize("pattern", ["all_atomic", "dense_middle", "update_edge_middle"])
 def test_kernel_split_of_survey_bytes_is_a_partition(pattern):
     """Every round's B_r goes to exactly one kernel class (the one consuming its arrivals), so
     the per-kernel SURVEY bytes the roofline uses add up to the whole-step figure."""
@@ -62,10 +62,11 @@ def test_kernel_split_of_survey_bytes_is_a_partition(pattern):
     n = len(ora)
     if pattern == "all_atomic":
         forms = [bench.ATOMIC] * n
-    else:  # sparse, one edge-store round, fused rounds, back to sparse
+    else:  # sparse, one edge-store round (or update + edge pushes in one pass), fused rounds,
+        # back to sparse
         forms = [bench.ATOMIC] * n
         lo, hi = n // 3, 2 * n // 3
-        forms[lo] = bench.EDGE
+        forms[lo] = bench.EDGE if pattern == "dense_middle" else bench.UPDATE_EDGE
         for i in range(lo + 1, hi):
             forms[i] = bench.FUSED
     rounds = rounds_of(ora, forms)
@@ -74,6 +75,13 @@ def test_kernel_split_of_survey_bytes_is_a_partition(pattern):
     assert sum(parts.values()) == whole
     if pattern == "dense_middle":
         assert parts["gossip_fused"] > 0 and parts["gossip_pull"] > 0 and parts["gossip_update"] > 0
+    elif pattern == "update_edge_middle":
+        # the update + push pass is timed as gossip_scatter_store: its round's B_r goes there
+        p, r = ora[lo - 1], ora[lo]
+        assert parts["gossip_scatter_store"] == (8 * p["relays"] + 8 * p["active_words"]
+                                                 + 4 * p["deg_active"] + 8 * p["active_vertices"]
+                                                 + 24 * r["active_words"]) > 0
+        assert parts["gossip_fused"] > 0 and parts["gossip_pull"] > 0
     else:
         assert parts["gossip_update"] == whole
 
