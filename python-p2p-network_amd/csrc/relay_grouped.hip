@@ -51,11 +51,6 @@ struct GroupedLds {
   uint8_t owner[64];                   // pick-window slot -> batch peer (churn only)
 };
 
-// lane-varying read of lane src's 64-bit value
-__device__ __forceinline__ int64_t readlane64_v(int64_t x, int src_lane) {
-  return (int64_t)bperm64(src_lane, (uint64_t)x);
-}
-
 __device__ __forceinline__ uint64_t bits_between(int lo, int hi) {  // bits [lo, hi), 0 <= lo, hi <= 64
   const uint64_t below_hi = hi >= 64 ? ~0ull : ((1ull << hi) - 1ull);
   const uint64_t below_lo = lo >= 64 ? ~0ull : ((1ull << lo) - 1ull);
@@ -65,7 +60,7 @@ __device__ __forceinline__ uint64_t bits_between(int lo, int hi) {  // bits [lo,
 // One batch's registers as it moves through the software pipeline (see the kernel).
 struct GStage {
   int b0, n;          // task peers b0 .. b0+n-1 (n = 0: no batch)
-  int64_t rb0, rb1;   // its adjacency slot range
+  uint32_t rb0, rb1;  // its adjacency slot range (slot ids fit 32 bits: rev[] holds them)
   uint64_t s;         // lane (g, w): seen word
   int32_t v;          // lane = slot of the first 64: neighbour id ...
   uint32_t rv;        // ... the receiver's slot of the connection (rev) ...
@@ -89,6 +84,10 @@ struct GStage {
 template <bool CHURN, int K, int LW, bool PO = false, bool PL = false>
 __global__ __launch_bounds__(256, P2PG_GROUPED_WAVES) void k_gossip_fused_grouped(DevGraph g, DevState st, RoundParams p) {
   using Lds = GroupedLds<LW>;
+  // never partitioned and never on a pre-update graph (the engine's dense rounds): the id
+  // translation and lost-slot tests fold away
+  g.gid = nullptr;
+  g.gone = nullptr;
   constexpr int WP = Lds::WP;
   constexpr int TS = Lds::TS;
   constexpr int GMAX = (64 >> LW) < 32 ? (64 >> LW) : 32;  // peers per batch
@@ -118,9 +117,9 @@ __global__ __launch_bounds__(256, P2PG_GROUPED_WAVES) void k_gossip_fused_groupe
   const int64_t ntasks = (V + 31) >> 5;
   uint64_t tot[STAT_N] = {0, 0, 0, 0, 0, 0, 0, 0};
 
-  for (int64_t task = (int64_t)blockIdx.x * WPB + wave_in_block(); task < ntasks;
-       task += (int64_t)gridDim.x * WPB) {
-    const int64_t u0 = task << 5;
+  for (int32_t task = (int32_t)blockIdx.x * WPB + wave_in_block(); task < ntasks;
+       task += (int32_t)gridDim.x * WPB) {
+    const int64_t u0 = (int64_t)task << 5;
     const uint32_t sat0 = PO ? 0u : st.S[task];
     const int nv = V - u0 < 32 ? (int)(V - u0) : 32;
     uint32_t todo = PO ? st.A[cur][task] : ~sat0;
@@ -130,8 +129,8 @@ __global__ __launch_bounds__(256, P2PG_GROUPED_WAVES) void k_gossip_fused_groupe
       if (!PO && lane == 0) st.A[cur][task] = 0u;
       continue;
     }
-    int64_t rp = 0;
-    if (lane <= nv) rp = g.rowptr[u0 + lane];
+    uint32_t rp = 0;  // lane l <= nv: rowptr[u0 + l] (32-bit slot ids)
+    if (lane <= nv) rp = (uint32_t)g.rowptr[u0 + lane];
     uint32_t c[STAT_N] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t aw = 0, sat = sat0;
     uint32_t rest = todo;
@@ -147,15 +146,15 @@ __global__ __launch_bounds__(256, P2PG_GROUPED_WAVES) void k_gossip_fused_groupe
       if (!rest) return;
       // the batch: <= GMAX consecutive peers and <= TS slots, or one wider peer
       const int b0 = __builtin_ctz(rest);
-      const int64_t rb0 = readlane64(rp, b0);
-      const bool fits = lane > b0 && lane <= b0 + GMAX && lane <= nv && rp - rb0 <= TS;
+      const uint32_t rb0 = (uint32_t)__builtin_amdgcn_readlane((int)rp, b0);
+      const bool fits = lane > b0 && lane <= b0 + GMAX && lane <= nv && rp - rb0 <= (uint32_t)TS;
       const int cnt = __popcll(__ballot(fits));
       const int n = cnt > 0 ? cnt : 1;
       rest &= (b0 + n >= 32 ? 0u : ~0u << (b0 + n));
       q.b0 = b0;
       q.n = n;
       q.rb0 = rb0;
-      q.rb1 = readlane64(rp, b0 + n);
+      q.rb1 = (uint32_t)__builtin_amdgcn_readlane((int)rp, b0 + n);
       const bool mine = gl < n && ((todo >> (b0 + gl)) & 1u);
       // PO: the peer's frontier row (its new receipts) instead of its seen row
       if (mine && wvalid) q.s = ld_once(&(PO ? Fc : st.seen)[(u0 + b0 + gl) * W + wl]);
@@ -165,10 +164,10 @@ __global__ __launch_bounds__(256, P2PG_GROUPED_WAVES) void k_gossip_fused_groupe
       int gj = 0;
       for (int i = 1; i < n; ++i)
         gj += (uint32_t)__builtin_amdgcn_readlane((int)rel, b0 + i) <= (uint32_t)lane;
-      q.rcv = rb0 + lane < q.rb1 && ((todo >> (b0 + gj)) & 1u);
+      q.rcv = rb0 + (uint32_t)lane < q.rb1 && ((todo >> (b0 + gj)) & 1u);
       if (q.rcv) {
-        q.v = ld_once(&g.colidx[rb0 + lane]);
-        q.rv = ld_once(&g.rev[rb0 + lane]);
+        q.v = ld_once(&g.colidx[rb0 + (uint32_t)lane]);
+        q.rv = ld_once(&g.rev[rb0 + (uint32_t)lane]);
       }
     };
     auto activity = [&](GStage& q) {
@@ -184,9 +183,9 @@ __global__ __launch_bounds__(256, P2PG_GROUPED_WAVES) void k_gossip_fused_groupe
       const bool mine = gl < q.n && ((todo >> (q.b0 + gl)) & 1u);
       return mine ? (PO ? ~0ull : fm & ~q.s) : 0ull;
     };
-    auto my_slots = [&](const GStage& q, int64_t cb) -> uint64_t {
+    auto my_slots = [&](const GStage& q, uint32_t cb) -> uint64_t {
       const int bi = gl < q.n ? q.b0 + gl : q.b0;
-      const int64_t lo = readlane64_v(rp, bi) - cb, hi = readlane64_v(rp, bi + 1) - cb;
+      const int64_t lo = (int64_t)bperm(bi, rp) - (int64_t)cb, hi = (int64_t)bperm(bi + 1, rp) - (int64_t)cb;
       return bits_between(lo < 0 ? 0 : (lo > 64 ? 64 : (int)lo), hi < 0 ? 0 : (hi > 64 ? 64 : (int)hi));
     };
     uint64_t X[GFG];
@@ -196,7 +195,7 @@ __global__ __launch_bounds__(256, P2PG_GROUPED_WAVES) void k_gossip_fused_groupe
       for (int qq = 0; qq < GFG; ++qq) o |= X[qq];
       return o;
     };
-    auto gathers = [&](int64_t cb, uint64_t& mg, uint64_t amv) {
+    auto gathers = [&](uint32_t cb, uint64_t& mg, uint64_t amv) {
 #pragma unroll
       for (int qq = 0; qq < GFG; ++qq) {
         const bool ok = mg != 0ull;
@@ -209,14 +208,14 @@ __global__ __launch_bounds__(256, P2PG_GROUPED_WAVES) void k_gossip_fused_groupe
           here = ok && ((a >> wl) & 1ull);
           pos = __popcll(a & ((1ull << wl) - 1ull));
         }
-        X[qq] = here ? __builtin_nontemporal_load(&Src[(cb + idx) * W + pos]) : 0ull;
+        X[qq] = here ? __builtin_nontemporal_load(&Src[(int64_t)(cb + (uint32_t)idx) * W + pos]) : 0ull;
       }
     };
-    auto active_slots = [&](const GStage& q, int64_t cb, int32_t v, bool rcv, uint32_t aword) -> uint64_t {
+    auto active_slots = [&](const GStage& q, uint32_t cb, int32_t v, bool rcv, uint32_t aword) -> uint64_t {
       bool act = rcv && ((aword >> (v & 31)) & 1u);
       if (CHURN && act) {
         int gj = 0;
-        for (int i = 1; i < q.n; ++i) gj += readlane64(rp, q.b0 + i) <= cb + lane;
+        for (int i = 1; i < q.n; ++i) gj += (uint32_t)__builtin_amdgcn_readlane((int)rp, q.b0 + i) <= cb + (uint32_t)lane;
         act = !churn_dropped((uint32_t)(p.round - 1), gidx(g, u0 + q.b0 + gj), gidx(g, v), p.churn_thr,
                              p.cseed_lo, p.cseed_hi);
       }
@@ -276,7 +275,7 @@ __global__ __launch_bounds__(256, P2PG_GROUPED_WAVES) void k_gossip_fused_groupe
           gathers(a.rb0, mg, a.amv);
           acc |= x_or();
         }
-        for (int64_t cb = a.rb0 + 64; cb < a.rb1; cb += 64) {  // one peer wider than 64 slots
+        for (uint32_t cb = a.rb0 + 64; cb < a.rb1; cb += 64) {  // one peer wider than 64 slots
           int32_t v = 0;
           uint32_t aword = 0;
           uint64_t amv = 0;
@@ -311,7 +310,7 @@ __global__ __launch_bounds__(256, P2PG_GROUPED_WAVES) void k_gossip_fused_groupe
       const int bi = gl < n ? a.b0 + gl : a.b0;
       const bool mine = gl < n && ((todo >> bi) & 1u);
       const int64_t u = u0 + bi;
-      const uint32_t degg = (uint32_t)(readlane64_v(rp, bi + 1) - readlane64_v(rp, bi));
+      const uint32_t degg = bperm(bi + 1, rp) - bperm(bi, rp);
       const uint64_t nw = acc & need;
       const uint64_t wm_all = __ballot(nw != 0ull);
       const uint32_t grp = (uint32_t)((wm_all >> (gl * WP)) & gmask);  // my peer's active words

@@ -1321,6 +1321,10 @@ template <bool CHURN, int K, int MODE = 0>
 __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph g, DevState st,
                                                                         RoundParams p) {
   constexpr bool PO = MODE == 1, UP = MODE == 2;
+  // never partitioned (local ids are the Philox ids) and never on a pre-update graph: known here,
+  // so the id translation and lost-slot tests fold away (fewer live scalar registers)
+  g.gid = nullptr;
+  g.gone = nullptr;
   __shared__ ScatterLds lds[WPB];
   const int lane = threadIdx.x & 63;
   const int wib = wave_in_block();
