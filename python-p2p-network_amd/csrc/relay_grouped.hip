@@ -115,7 +115,10 @@ __global__ __launch_bounds__(256, P2PG_GROUPED_WAVES) void k_gossip_fused_groupe
   const uint64_t fm = wvalid ? full_mask(wl, W, st.M) : 0ull;
   const uint64_t gmask = (1ull << WP) - 1ull;
   const int64_t ntasks = (V + 31) >> 5;
-  uint64_t tot[STAT_N] = {0, 0, 0, 0, 0, 0, 0, 0};
+  // wave totals in 32 bits (8 fewer scalar registers): a wave of a balanced grid (<= 32 x the
+  // resident blocks) covers few tasks -- c4: ~2.4 -- so even 10^9 peers keep its relay / wedge
+  // sums (<= tasks x 32 peers x 4096 messages x fanout 16; hubs excluded) far below 2^32
+  uint32_t tot[STAT_N] = {0, 0, 0, 0, 0, 0, 0, 0};
 
   for (int32_t task = (int32_t)blockIdx.x * WPB + wave_in_block(); task < ntasks;
        task += (int32_t)gridDim.x * WPB) {

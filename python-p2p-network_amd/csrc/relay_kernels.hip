@@ -1340,7 +1340,10 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
   const uint64_t fm = valid ? full_mask(lane, W, st.M) : 0ull;
   // per-lane counters are 32-bit and per task (<= 32 peers, none a hub: no overflow), folded
   // into wave-uniform 64-bit totals after each task (fewer live VGPRs than 64-bit lanes)
-  uint64_t tot[STAT_N] = {0, 0, 0, 0, 0, 0, 0, 0};
+  // wave totals in 32 bits (8 fewer scalar registers): a wave of a balanced grid (<= 32 x the
+  // resident blocks) covers few tasks -- c4: ~2.4 -- so even 10^9 peers keep its relay / wedge
+  // sums (<= tasks x 32 peers x 4096 messages x fanout 16; hubs excluded) far below 2^32
+  uint32_t tot[STAT_N] = {0, 0, 0, 0, 0, 0, 0, 0};
   PROF_DECL
 
   // Issuer (wave-uniform): this wave's tasks in grid-stride order and, in each, its
@@ -1599,7 +1602,8 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
     if (!PO && nw) {
       st_frow(&st.seen[u * W + lane], a.s | nw);
       const uint32_t pc = (uint32_t)__popcll(nw);
-      const uint32_t per_bit = deg < (uint64_t)p.fanout ? (uint32_t)deg : (uint32_t)p.fanout;
+      const uint32_t kf = K > 0 ? (uint32_t)K : (uint32_t)p.fanout;
+      const uint32_t per_bit = deg < (uint64_t)kf ? (uint32_t)deg : kf;
       c[ST_NEW] += pc;
       c[ST_RELAYS] += pc * per_bit;
       c[ST_ACTIVE_W] += 1;
