@@ -191,12 +191,10 @@ struct PullStage {
 // One target's prefetch stage for k_gossip_fused: as PullStage, with 32-bit peer and slot ids
 // (gossip slot ids are uint32: rev[]) -- the fused kernel's scalar registers are the scarce ones.
 struct FusedStage {
-  int b;            // 0 = a target, -1 = none
-  int32_t u;        // the target peer
+  int32_t u;        // the target peer (-1: none)
   uint32_t beg, end;
   uint64_t s;
   int32_t v;        // (the E row of slot j is row j itself: no per-lane row id is kept)
-  bool act;
   uint32_t aword;
   uint64_t mr;
   uint64_t am;
@@ -1398,12 +1396,10 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
   };
 
   auto issue = [&](FusedStage& q) {
-    q.act = false;
     q.v = 0;
     q.rv = 0;
     q.s = 0;
     q.u = next_peer(q.beg, q.end);
-    q.b = q.u < 0 ? -1 : 0;
     if (q.u < 0) return;
     // PO: the peer's frontier row (its new receipts of this round) instead of its seen row;
     // UP: the seen row and, in the stage's mask field, the push row (the arrivals)
@@ -1417,7 +1413,7 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
   };
   // loads only; gather() tests the bit (see k_pull1)
   auto activity = [&](FusedStage& q) {
-    if (MODE != 0 || q.b < 0) return;
+    if (MODE != 0 || q.u < 0) return;
     const uint32_t j = q.beg + lane;
     q.am = 0;
     q.aword = 0;
@@ -1517,7 +1513,7 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
   issue(sA);
   issue(sB);
   activity(sA);
-  if (sA.b >= 0) gather(sA, sA.mr);
+  if (sA.u >= 0) gather(sA, sA.mr);
   activity(sB);
   issue(sC);
   PROF_MARK(5);
@@ -1593,7 +1589,7 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
     flush_pending();
     // advance the pipeline before this target's stores and picks: gathers of t+1 (their
     // activity words were loaded a target ago), activity words of t+2, rows of t+3
-    if (b.b >= 0) gather(b, b.mr);
+    if (b.u >= 0) gather(b, b.mr);
     activity(cc);
     issue(d);
     PROF_MARK(2);
@@ -1652,13 +1648,13 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
     if (!PO && !__ballot(valid && (a.s | nw) != fm)) nsat |= 1u << (u & 31);
   };
   for (;;) {
-    if (sA.b < 0) break;
+    if (sA.u < 0) break;
     step(sA, sB, sC, sD);
-    if (sB.b < 0) break;
+    if (sB.u < 0) break;
     step(sB, sC, sD, sA);
-    if (sC.b < 0) break;
+    if (sC.u < 0) break;
     step(sC, sD, sA, sB);
-    if (sD.b < 0) break;
+    if (sD.u < 0) break;
     step(sD, sA, sB, sC);
   }
   flush_pending();
