@@ -49,6 +49,8 @@ def calib(d):
 def cls(name):
     """rocprof kernel name -> bench.py timer class (include/p2pgpu.h P2PG_KCLASS_N)."""
     tmpl = name.split("<", 1)[1].split(">(")[0] if "<" in name else ""
+    if "k_gossip_fused" in name and tmpl.count(",") >= 2 and tmpl.rsplit(",", 1)[1].strip() in ("1", "2"):
+        return "gossip_scatter_store"  # push-only / update+push modes (timed with the store pushes)
     if "k_gossip_fused" in name or "k_wide_zero" in name or "k_wide_push" in name:
         return "gossip_fused"  # (the hub pushes ride in the fused rounds' timed launch group)
     if any(x in name for x in ("k_sparse_words", "k_chunk_scan", "k_sparse_push", "k_touched_bits")):
