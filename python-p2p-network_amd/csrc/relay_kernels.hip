@@ -232,6 +232,27 @@ __device__ __forceinline__ uint64_t src_word_m(const uint64_t* __restrict__ Src,
   return x;
 }
 
+// Two packed E-row slices per load for rows of W <= 32 words (k_gossip_fused<.., HALF>): lanes
+// 0-31 read slot row r0, lanes 32-63 slot row r1, each at its word's packed position (m0 / m1 =
+// the two senders' active words, h0 / h1 = the words to read).  A one-slot load leaves half the
+// wave idle at these widths, and every slot costs the same wave-level setup.
+__device__ __forceinline__ uint64_t src_word_pair(const uint64_t* __restrict__ Src, uint32_t r0,
+                                                  uint32_t r1, int W, uint32_t m0, uint32_t m1,
+                                                  uint32_t h0, uint32_t h1) {
+  uint64_t x = 0ull;
+  if (__builtin_amdgcn_inverse_ballot_w64((uint64_t)h0 | ((uint64_t)h1 << 32))) {
+    const bool lo = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) < 32u;
+    const uint32_t pos = __builtin_amdgcn_mbcnt_hi(m1, __builtin_amdgcn_mbcnt_lo(lo ? m0 : 0u, 0u));
+    const uint32_t row = lo ? r0 : r1;
+#if P2PG_NT_LOADS
+    x = __builtin_nontemporal_load(&Src[(int64_t)row * W + pos]);
+#else
+    x = Src[(int64_t)row * W + pos];
+#endif
+  }
+  return x;
+}
+
 // Same computation as k_pull for W <= 64 (one row slice), software-pipelined two targets
 // deep so that a target costs ~one memory round trip instead of five: the task's 33 row
 // offsets come in one load; target t+2's seen word and first neighbour chunk are issued, and
@@ -1315,7 +1336,8 @@ constexpr int FG = P2PG_FG;
 // are the touched non-hub peers (T[r&1]), their arrivals the row pushes next[r&1] of the sparse
 // round before (read and cleared), then dedup, frontier row, bitmaps, counters and the pushes as
 // in a fused round; the touched hubs are left in T for a hub-only update (launch_gossip_update_push).
-template <bool CHURN, int K, int MODE = 0>
+// HALF (MODE 0, W <= 32): arrivals gathered two slots per load (src_word_pair).
+template <bool CHURN, int K, int MODE = 0, bool HALF = false>
 __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph g, DevState st,
                                                                         RoundParams p) {
   constexpr bool PO = MODE == 1, UP = MODE == 2;
@@ -1436,6 +1458,34 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
     const uint64_t needm = __ballot((fm & ~q.s) != 0ull);
     const uint32_t jq = q.beg + lane;
     uint64_t m = __ballot(jq < q.end && ((q.aword >> (q.v & 31)) & 1u));
+    if constexpr (HALF) {  // FG slots in flight, two per load (FG / 2 loads)
+      constexpr int FH = FG / 2;
+      uint32_t r0[FH], r1[FH], m0[FH], m1[FH];
+#pragma unroll
+      for (int k = FH; k < FG; ++k) X[k] = 0ull;
+#pragma unroll
+      for (int k = 0; k < FH; ++k) {
+        r0[k] = r1[k] = m0[k] = m1[k] = 0u;
+        if (m) {
+          const int i0 = __builtin_ctzll(m);
+          m &= m - 1ull;
+          r0[k] = q.beg + (uint32_t)i0;
+          m0[k] = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)q.am, i0);
+        }
+        if (m) {
+          const int i1 = __builtin_ctzll(m);
+          m &= m - 1ull;
+          r1[k] = q.beg + (uint32_t)i1;
+          m1[k] = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)q.am, i1);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < FH; ++k)
+        X[k] = src_word_pair(Src, r0[k], r1[k], W, m0[k], m1[k], m0[k] & (uint32_t)needm,
+                             m1[k] & (uint32_t)needm);
+      mr = m;
+      return;
+    }
     // all slot ids / word masks first, then all FG loads back to back: a readlane between
     // two loads would make the wave wait for the first one (merged vmcnt state)
     uint32_t sv[FG];
@@ -1538,7 +1588,33 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
       uint64_t sam = a.am;
       uint32_t cb = a.beg;
       for (;;) {
-        while (m) {
+        while (HALF && m) {  // 8 slots per trip, two per load
+          uint32_t r0[4], r1[4], m0[4], m1[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            r0[k] = r1[k] = m0[k] = m1[k] = 0u;
+            if (m) {
+              const int i0 = __builtin_ctzll(m);
+              m &= m - 1ull;
+              r0[k] = cb + (uint32_t)i0;
+              m0[k] = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)sam, i0);
+            }
+            if (m) {
+              const int i1 = __builtin_ctzll(m);
+              m &= m - 1ull;
+              r1[k] = cb + (uint32_t)i1;
+              m1[k] = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)sam, i1);
+            }
+          }
+          uint64_t x[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            x[k] = src_word_pair(Src, r0[k], r1[k], W, m0[k], m1[k], m0[k] & (uint32_t)needm,
+                                 m1[k] & (uint32_t)needm);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) acc |= x[k];
+        }
+        while (!HALF && m) {
           uint32_t sv[8];
           uint64_t am[8];
           bool ok[8];
@@ -1582,6 +1658,7 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
     // wait would stall until those gathers return).
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     PROF_MARK(1);
+    if (HALF) acc |= bperm64(lane ^ 32, acc);  // lanes 32-63 gathered for words 0-31 too
     if (UP && acc) {  // the push row is consumed: all-zero again outside touched rows
       st_prow(&st.next[cur][(int64_t)u * W + lane], 0ull);
       c[ST_AUX] += 1;  // touched (pushed-to) words consumed
@@ -2189,10 +2266,23 @@ hipError_t launch_gossip_fused(const DevGraph& g, const DevState& st, const Roun
     hipError_t r = launch_gossip_fused_grouped(g, st, p, s);
     if (r != hipSuccess) return r;
   } else {
-#define P2PG_FUSED(CH, KK)                                                                   \
-  hipLaunchKernelGGL((k_gossip_fused<CH, KK>),                                             \
-                     dim3(balanced_grid(k_gossip_fused<CH, KK>, (g.V + 31) >> 5)), dim3(256), 0, \
-                     s, g, st, p)
+#define P2PG_FUSED(CH, KK)                                                                       \
+  do {                                                                                         \
+    if (half)                                                                                  \
+      hipLaunchKernelGGL((k_gossip_fused<CH, KK, 0, true>),                                    \
+                         dim3(balanced_grid(k_gossip_fused<CH, KK, 0, true>, (g.V + 31) >> 5)), \
+                         dim3(256), 0, s, g, st, p);                                           \
+    else                                                                                       \
+      hipLaunchKernelGGL((k_gossip_fused<CH, KK>),                                             \
+                         dim3(balanced_grid(k_gossip_fused<CH, KK>, (g.V + 31) >> 5)), dim3(256), \
+                         0, s, g, st, p);                                                      \
+  } while (0)
+  // W <= 32: two slots per gather load (P2PG_FUSED_HALF=0: one, A/B only)
+  static const bool half_on = [] {
+    const char* e = std::getenv("P2PG_FUSED_HALF");
+    return !(e && std::strcmp(e, "0") == 0);
+  }();
+  const bool half = half_on && st.W <= 32;
   const bool ch = p.churn_thr != 0;
   switch (p.fanout) {
     case 1: if (ch) P2PG_FUSED(true, 1); else P2PG_FUSED(false, 1); break;
