@@ -632,10 +632,15 @@ __global__ __launch_bounds__(256) void k_gossip_update(DevGraph g, DevState st,
 // k_gossip_update (every gossip test runs it).
 struct UpdStage {
   int64_t u;   // touched peer (-1: none)
+  int64_t u2;  // PAIR: a second touched peer of the same task (-1: none)
   uint64_t x;  // this lane's push word
   uint64_t s;  // this lane's seen word (where x != 0)
 };
 
+// PAIR (W <= 32): two touched peers of a task per stage, lanes 0-31 the first, 32-63 the second
+// (one peer per wave leaves half the wave idle at these widths and pays the per-peer wave work
+// once per peer).
+template <bool PAIR = false>
 __global__ __launch_bounds__(256) void k_gossip_update1(DevGraph g, DevState st, RoundParams p) {
   const int lane = threadIdx.x & 63;
   const int wib = wave_in_block();
@@ -646,7 +651,9 @@ __global__ __launch_bounds__(256) void k_gossip_update1(DevGraph g, DevState st,
   uint64_t* __restrict__ Fc = st.F[cur];
   uint32_t* __restrict__ Tc = st.T[cur];
   const int64_t ntasks = (V + 31) >> 5;
-  const bool valid = lane < W;
+  const int hl = PAIR ? lane >> 5 : 0;      // PAIR: which peer of the stage this lane serves
+  const int wl = PAIR ? lane & 31 : lane;   // ... and its word
+  const bool valid = wl < W;
   uint64_t c[STAT_N] = {0, 0, 0, 0, 0, 0, 0, 0};
 
   const int64_t tstride = (int64_t)gridDim.x * WPB;
@@ -676,12 +683,15 @@ __global__ __launch_bounds__(256) void k_gossip_update1(DevGraph g, DevState st,
   };
   auto issue_x = [&](UpdStage& q) {
     q.u = next_peer();
+    q.u2 = (PAIR && q.u >= 0 && it_rest) ? next_peer() : -1;  // never across a task boundary
     q.x = 0;
     q.s = 0;
-    if (q.u >= 0 && valid) q.x = nx[q.u * W + lane];
+    const int64_t me = hl ? q.u2 : q.u;
+    if (me >= 0 && valid) q.x = nx[me * W + wl];
   };
   auto issue_s = [&](UpdStage& q) {
-    if (q.u >= 0 && q.x) q.s = st.seen[q.u * W + lane];
+    const int64_t me = hl ? q.u2 : q.u;
+    if (me >= 0 && q.x) q.s = st.seen[me * W + wl];
   };
 
   int64_t ct = -1;  // task of the consumed peers
@@ -691,26 +701,30 @@ __global__ __launch_bounds__(256) void k_gossip_update1(DevGraph g, DevState st,
     aw = 0;
   };
   auto consume = [&](const UpdStage& q) {
-    const int64_t u = q.u;
-    if ((u >> 5) != ct) {
+    if ((q.u >> 5) != ct) {
       finish_task();
-      ct = u >> 5;
+      ct = q.u >> 5;
     }
-    const int64_t deg = ldc(g.rowptr + u + 1) - ldc(g.rowptr + u);
+    const int64_t u = hl ? q.u2 : q.u;  // this lane's peer (PAIR: the stage's second one above 32)
+    const int64_t deg1 = ldc(g.rowptr + q.u + 1) - ldc(g.rowptr + q.u);
+    const int64_t deg2 = PAIR && q.u2 >= 0 ? ldc(g.rowptr + q.u2 + 1) - ldc(g.rowptr + q.u2) : 0;
+    const int64_t deg = hl ? deg2 : deg1;
     // relays per first receipt: gossip min(k, deg); flood (rows materialized by a topology
     // update) deg - 1, the sender's connection being excluded (node.py:106-112)
     const uint64_t fan = p.mode == 0 ? (uint64_t)(deg > 0 ? deg - 1 : 0)
                                      : (uint64_t)(deg < p.fanout ? deg : p.fanout);
     const uint64_t x = q.x, s = q.s;
     if (x) {
-      st_prow(&nx[u * W + lane], 0ull);
+      st_prow(&nx[u * W + wl], 0ull);
       c[ST_AUX] += 1;  // touched (pushed-to) words consumed
     }
     const uint64_t nw = x & ~s;
-    const uint64_t wm = __ballot(nw != 0ull);
-    if (wm && st.AW[cur] && lane == 0) st.AW[cur][u] = wm;
-    if (nw) st_prow(&st.seen[u * W + lane], s | nw);
-    if (valid && wm) st_prow(&Fc[u * W + lane], nw);
+    const uint64_t wmb = __ballot(nw != 0ull);
+    const uint64_t wm1 = PAIR ? (wmb & 0xFFFFFFFFull) : wmb, wm2 = PAIR ? (wmb >> 32) : 0ull;
+    const uint64_t wm = hl ? wm2 : wm1;  // this lane's peer's new words
+    if (wm && st.AW[cur] && wl == 0) st.AW[cur][u] = wm;
+    if (nw) st_prow(&st.seen[u * W + wl], s | nw);
+    if (valid && wm) st_prow(&Fc[u * W + wl], nw);
     if (nw) {
       const uint64_t pc = (uint64_t)__popcll(nw);
       c[ST_NEW] += pc;
@@ -718,12 +732,11 @@ __global__ __launch_bounds__(256) void k_gossip_update1(DevGraph g, DevState st,
       c[ST_ACTIVE_W] += 1;
       c[ST_WEDGES] += (uint64_t)deg;
     }
-    if (wm) {
-      aw |= 1u << (u & 31);
-      if (lane == 0) {
-        c[ST_ACTIVE_V] += 1;
-        c[ST_DEG_ACT] += (uint64_t)deg;
-      }
+    if (wm1) aw |= 1u << (q.u & 31);
+    if (wm2) aw |= 1u << (q.u2 & 31);
+    if (wm && wl == 0) {
+      c[ST_ACTIVE_V] += 1;
+      c[ST_DEG_ACT] += (uint64_t)deg;
     }
   };
   // three stages rotate by unrolling (a register copy of a load in flight would wait for it)
@@ -2087,6 +2100,15 @@ hipError_t launch_materialize(const DevGraph& g, const DevState& st, const Round
   return hipGetLastError();
 }
 
+// W <= 32 rows: two touched peers per stage of the pipelined update (P2PG_UPDATE_PAIR=0: one)
+static bool update_pair_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("P2PG_UPDATE_PAIR");
+    return !(e && std::strcmp(e, "0") == 0);
+  }();
+  return on;
+}
+
 hipError_t launch_gossip_update(const DevGraph& g, const DevState& st, const RoundParams& p,
                                 hipStream_t s) {
   // blocks cap (P2PG_UPDATE_GRID): c4 A/B, interleaved, update ms per step: 256 / 512 / 1024 /
@@ -2119,8 +2141,10 @@ hipError_t launch_gossip_update(const DevGraph& g, const DevState& st, const Rou
       case 4: hipLaunchKernelGGL(k_gossip_update_g<4>, dim3(grid), dim3(256), 0, s, g, st, p); break;
       default: hipLaunchKernelGGL(k_gossip_update_g<5>, dim3(grid), dim3(256), 0, s, g, st, p); break;
     }
+  } else if (st.W <= 32 && pipelined && update_pair_on()) {
+    hipLaunchKernelGGL(k_gossip_update1<true>, dim3(grid), dim3(256), 0, s, g, st, p);
   } else if (st.W <= 64 && pipelined)
-    hipLaunchKernelGGL(k_gossip_update1, dim3(grid), dim3(256), 0, s, g, st, p);
+    hipLaunchKernelGGL(k_gossip_update1<false>, dim3(grid), dim3(256), 0, s, g, st, p);
   else
     hipLaunchKernelGGL(k_gossip_update, dim3(grid), dim3(256), 0, s, g, st, p);
   return hipGetLastError();
@@ -2243,7 +2267,7 @@ hipError_t launch_gossip_update_push(const DevGraph& g, const DevState& st, cons
     ph.border = g.H;
     ph.phase = 1;
     const int grid = (int)std::min<int64_t>(grid_tasks((g.V + 31) >> 5), 1024);
-    hipLaunchKernelGGL(k_gossip_update1, dim3(grid), dim3(256), 0, s, g, st, ph);
+    hipLaunchKernelGGL(k_gossip_update1<false>, dim3(grid), dim3(256), 0, s, g, st, ph);
     r = hipGetLastError();
     if (r != hipSuccess) return r;
   }
