@@ -839,6 +839,146 @@ __global__ __launch_bounds__(256) void k_gossip_update_g(DevGraph g, DevState st
   flush_stats(st.stats, c, lane);
 }
 
+// The update for rows of W <= 16 words, pipelined like k_gossip_update1: G = 64 / WP touched peers
+// of one task per stage (lane = (peer g, word w), WP = W rounded up to a power of two), three
+// stages in flight (push rows + row offsets of t+2, seen words of t+1, consume t).  Each lane
+// carries its stage peer's id, so a stage costs no scalar registers per peer.  Same results as
+// k_gossip_update.
+struct UpdStageG {
+  int32_t t;   // task of the stage's peers (-1: no peers)
+  int32_t me;  // this lane's peer (-1: none)
+  uint64_t x;  // its push word
+  uint64_t s;  // its seen word (where x != 0)
+  uint32_t r0, r1;  // its peer's slot range (relays / wedges)
+};
+
+template <int LW>
+__global__ __launch_bounds__(256) void k_gossip_update_gp(DevGraph g, DevState st, RoundParams p) {
+  constexpr int WP = 1 << LW, G = 64 >> LW;
+  const int lane = threadIdx.x & 63;
+  const int wib = wave_in_block();
+  const int W = st.W;
+  const int cur = p.round & 1;
+  uint64_t* __restrict__ nx = st.next[cur];
+  uint64_t* __restrict__ Fc = st.F[cur];
+  uint32_t* __restrict__ Tc = st.T[cur];
+  uint64_t* __restrict__ AWc = st.AW[cur];
+  const int32_t ntasks = (int32_t)((g.V + 31) >> 5);
+  const int grp = lane >> LW, w = lane & (WP - 1);
+  const bool wvalid = w < W;
+  const uint64_t segm = WP >= 64 ? ~0ull : (1ull << WP) - 1ull;
+  uint64_t c[STAT_N] = {0, 0, 0, 0, 0, 0, 0, 0};
+
+  const int32_t tstride = (int32_t)gridDim.x * WPB;
+  int32_t pf_task = (int32_t)blockIdx.x * WPB + wib;
+  uint32_t pf_tw = pf_task < ntasks ? ldc(&Tc[pf_task]) : 0u;
+  int32_t it_task = 0;
+  uint32_t it_rest = 0;
+  auto next_task = [&]() -> bool {  // make it_rest the next task's touched peers (false: none left)
+    while (!it_rest) {
+      const int32_t t = pf_task;
+      if (t >= ntasks) return false;
+      const uint32_t tw0 = pf_tw;
+      pf_task = t + tstride;
+      pf_tw = pf_task < ntasks ? ldc(&Tc[pf_task]) : 0u;
+      const uint32_t tw = tw0 & phase_mask(p, t);
+      if (!tw) {
+        if (lane == 0 && p.phase != 1) st.A[cur][t] = 0u;  // put_active(.., 0, ..)
+        continue;
+      }
+      if (lane == 0) Tc[t] = tw0 & ~tw;  // consumed (the other phase's bits stay)
+      it_task = t;
+      it_rest = tw;
+    }
+    return true;
+  };
+  auto issue_x = [&](UpdStageG& q) {
+    q.t = -1;
+    q.me = -1;
+    q.x = 0;
+    q.s = 0;
+    q.r0 = q.r1 = 0;
+    if (!next_task()) return;
+    q.t = it_task;
+    // up to G peers of this task, lowest first: group g takes the g-th remaining bit
+    const uint32_t n = (uint32_t)__popc(it_rest);
+    const uint32_t take = n < (uint32_t)G ? n : (uint32_t)G;
+    if ((uint32_t)grp < take) q.me = (it_task << 5) + (int32_t)select_bit32(it_rest, (uint32_t)grp);
+    // the rest of the task: its bits from the (take)-th on
+    it_rest = take >= n ? 0u : it_rest & ~((1u << select_bit32(it_rest, take)) - 1u);
+    if (q.me >= 0) {
+      if (wvalid) q.x = nx[(int64_t)q.me * W + w];
+      q.r0 = (uint32_t)g.rowptr[q.me];
+      q.r1 = (uint32_t)g.rowptr[q.me + 1];
+    }
+  };
+  auto issue_s = [&](UpdStageG& q) {
+    if (q.me >= 0 && q.x) q.s = st.seen[(int64_t)q.me * W + w];
+  };
+  auto consume = [&](const UpdStageG& q) {
+    const int64_t u = q.me;
+    const uint64_t x = q.x, s = q.s;
+    if (x) {
+      st_prow(&nx[u * W + w], 0ull);
+      c[ST_AUX] += 1;  // touched (pushed-to) words consumed
+    }
+    const uint64_t nw = x & ~s;
+    const uint64_t wm = (__ballot(nw != 0ull) >> (grp * WP)) & segm;  // this peer's new words
+    if (nw) st_prow(&st.seen[u * W + w], s | nw);
+    if (q.me >= 0 && wvalid && wm) st_prow(&Fc[u * W + w], nw);
+    uint32_t bit = 0;
+    if (wm) {
+      const int64_t deg = (int64_t)(q.r1 - q.r0);
+      // relays per first receipt: gossip min(k, deg); flood (rows materialized by a topology
+      // update) deg - 1, the sender's connection being excluded (node.py:106-112)
+      const uint64_t fan = p.mode == 0 ? (uint64_t)(deg > 0 ? deg - 1 : 0)
+                                       : (uint64_t)(deg < p.fanout ? deg : p.fanout);
+      if (nw) {
+        const uint64_t pc = (uint64_t)__popcll(nw);
+        c[ST_NEW] += pc;
+        c[ST_RELAYS] += pc * fan;
+        c[ST_ACTIVE_W] += 1;
+        c[ST_WEDGES] += (uint64_t)deg;
+      }
+      if (w == 0) {
+        if (AWc) AWc[u] = wm;
+        c[ST_ACTIVE_V] += 1;
+        c[ST_DEG_ACT] += (uint64_t)deg;
+        bit = 1u << (u & 31);
+      }
+    }
+    // distinct bits per peer: the wave sum of the w == 0 lanes' bits is their OR
+    return wave_reduce_u32<false>(bit);
+  };
+  int32_t ct = -1;  // task of the consumed stages
+  uint32_t aw = 0;
+  auto step = [&](UpdStageG& a, UpdStageG& b, UpdStageG& cc) {
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): a's seen words and b's push rows landed
+    issue_s(b);
+    issue_x(cc);
+    if (a.t != ct) {
+      if (ct >= 0 && lane == 0) put_active(st.A[cur], ct, aw, p);
+      aw = 0;
+      ct = a.t;
+    }
+    aw |= consume(a);
+  };
+  UpdStageG sA, sB, sC;
+  issue_x(sA);
+  issue_x(sB);
+  issue_s(sA);
+  for (;;) {
+    if (sA.t < 0) break;
+    step(sA, sB, sC);
+    if (sB.t < 0) break;
+    step(sB, sC, sA);
+    if (sC.t < 0) break;
+    step(sC, sA, sB);
+  }
+  if (ct >= 0 && lane == 0) put_active(st.A[cur], ct, aw, p);
+  flush_stats(st.stats, c, lane);
+}
+
 // Messages in flight after round r = p.round - 1, as row pushes into next[p.round&1] + T bits
 // (the form k_gossip_update consumes), one wave per receiver u, lane = word, serial over u's
 // slots (not a hot path):
@@ -2130,7 +2270,16 @@ hipError_t launch_gossip_update(const DevGraph& g, const DevState& st, const Rou
   // several touched peers per wave up to W = 16; at W = 32 (two per wave) the pipelined
   // one-peer kernel is faster (c4 --msgs 2048, profiles/r03/ab_update_g.txt: 20.4 vs 19.65 ms;
   // W = 16: 10.25 vs 13.95 ms, W = 8: 6.75 vs 12.1 ms)
-  if (narrow && st.W <= 16) {
+  static const bool gp = [] {  // P2PG_UPDATE_GP=0: the unpipelined grouped update at W <= 16 (A/B)
+    const char* e = std::getenv("P2PG_UPDATE_GP");
+    return !(e && std::strcmp(e, "0") == 0);
+  }();
+  if (narrow && gp && st.W > 4 && st.W <= 16) {
+    if (st.W <= 8)
+      hipLaunchKernelGGL(k_gossip_update_gp<3>, dim3(grid), dim3(256), 0, s, g, st, p);
+    else
+      hipLaunchKernelGGL(k_gossip_update_gp<4>, dim3(grid), dim3(256), 0, s, g, st, p);
+  } else if (narrow && st.W <= 16) {
     int lw = 0;
     while ((1 << lw) < st.W) ++lw;
     switch (lw) {
