@@ -1489,11 +1489,16 @@ constexpr int FG = P2PG_FG;
 // are the touched non-hub peers (T[r&1]), their arrivals the row pushes next[r&1] of the sparse
 // round before (read and cleared), then dedup, frontier row, bitmaps, counters and the pushes as
 // in a fused round; the touched hubs are left in T for a hub-only update (launch_gossip_update_push).
+// MODE 3, PL (pull only): the last dense round before the sparse ones (32 < W <= 64) -- arrivals,
+// dedup, frontier rows and bitmaps as in MODE 0, no picks and no E stores (the round's pushes go by
+// row atomics afterwards); the software pipeline runs across task boundaries, which k_pull1's
+// per-task three-stage pipeline does not.
 // HALF (MODE 0, W <= 32): arrivals gathered two slots per load (src_word_pair).
 template <bool CHURN, int K, int MODE = 0, bool HALF = false>
 __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph g, DevState st,
                                                                         RoundParams p) {
-  constexpr bool PO = MODE == 1, UP = MODE == 2;
+  constexpr bool PO = MODE == 1, UP = MODE == 2, PL = MODE == 3;
+  constexpr bool GATHER = MODE == 0 || PL;  // arrivals gathered from E
   // never partitioned (local ids are the Philox ids) and never on a pre-update graph: known here,
   // so the id translation and lost-slot tests fold away (fewer live scalar registers)
   g.gid = nullptr;
@@ -1582,13 +1587,13 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
     if (UP) q.am = valid ? st.next[cur][(int64_t)q.u * W + lane] : 0ull;
     const uint32_t j = q.beg + lane;
     if (j < q.end) {
-      if (MODE == 0) q.v = ld_once(&g.colidx[j]);
-      q.rv = ld_once(&g.rev[j]);
+      if (GATHER) q.v = ld_once(&g.colidx[j]);
+      if (!PL) q.rv = ld_once(&g.rev[j]);
     }
   };
   // loads only; gather() tests the bit (see k_pull1)
   auto activity = [&](FusedStage& q) {
-    if (MODE != 0 || q.u < 0) return;
+    if (!GATHER || q.u < 0) return;
     const uint32_t j = q.beg + lane;
     q.am = 0;
     q.aword = 0;
@@ -1602,7 +1607,7 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
   // first 64) still to gather
   uint64_t X[FG];
   auto gather = [&](const FusedStage& q, uint64_t& mr) {
-    if (MODE != 0) {  // no arrivals to gather: they came with the row stage
+    if (!GATHER) {  // no arrivals to gather: they came with the row stage
 #pragma unroll
       for (int k = 0; k < FG; ++k) X[k] = 0ull;
       mr = 0;
@@ -1736,7 +1741,7 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
     for (int k = 0; k < FG; ++k) acc |= X[k];
     if (UP) acc = a.am;  // the push row
     PROF_MARK(0);
-    if (MODE == 0) {
+    if (GATHER) {
       uint64_t m = a.mr;  // the rest of the first 64 slots, then further 64-slot chunks
       uint64_t sam = a.am;
       uint32_t cb = a.beg;
@@ -1850,7 +1855,9 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
       // every 4 chunks and wait for them right there -- a load that MAY be in flight when
       // the picks read the slots would make the compiler wait for everything, the next
       // target's gathers included.
-      if (deg <= (uint64_t)GCHUNK) {
+      if (PL) {
+        // (no pushes: the sparse push that follows reads the frontier row)
+      } else if (deg <= (uint64_t)GCHUNK) {
         scatter_row<CHURN, K, true, 1>(g, st, p, lds[wib], lane, u, a.beg, (int64_t)deg, 0, 0,
                                        nw, a.rv, 0, c PROF_PASS);
         pend = true;
@@ -2225,6 +2232,27 @@ hipError_t launch_gossip_pull(const DevGraph& g, const DevState& st, const Round
     if (hp.n_hubs)
       hipLaunchKernelGGL((k_pull_hub_finalize<true>), dim3(grid_tasks(hp.n_hubs)), dim3(256), 0,
                          s, g, st, p, hp);
+    return hipGetLastError();
+  }
+  // wider packed rows: the pull-only mode of the fused kernel (its pipeline crosses task
+  // boundaries); P2PG_FUSED_PULL=0 keeps k_pull1 (A/B only)
+  static const bool fused_pull = [] {
+    const char* e = std::getenv("P2PG_FUSED_PULL");
+    return !(e && std::strcmp(e, "0") == 0);
+  }();
+  if (fused_pull && st.W > GROUPED_PULL_W_MAX && st.W <= 64 && st.AW[(p.round & 1) ^ 1] &&
+      p.phase < 0) {
+    RoundParams pp = p;
+    pp.store_f = 1;  // the sparse push of this round reads the frontier rows
+    if (hp.n_items)
+      hipLaunchKernelGGL((k_pull_hub_partial<false, true>), dim3(grid_tasks(hp.n_items)),
+                         dim3(256), 0, s, g, st, pp, hp);
+    hipLaunchKernelGGL((k_gossip_fused<false, 3, 3>),
+                       dim3(balanced_grid(k_gossip_fused<false, 3, 3>, (g.V + 31) >> 5)), dim3(256),
+                       0, s, g, st, pp);
+    if (hp.n_hubs)
+      hipLaunchKernelGGL((k_pull_hub_finalize<true>), dim3(grid_tasks(hp.n_hubs)), dim3(256), 0,
+                         s, g, st, pp, hp);
     return hipGetLastError();
   }
   return pull_with_hubs<false, true>(g, st, p, hp, s);
