@@ -2221,6 +2221,33 @@ static bool grouped_pull_enabled() {
 
 hipError_t launch_gossip_pull(const DevGraph& g, const DevState& st, const RoundParams& p,
                               const HubPlan& hp, hipStream_t s) {
+  // packed rows (8 < W <= 64): the pull-only mode of the fused kernel (its pipeline crosses task
+  // boundaries; W <= 32: two slots per gather load); P2PG_FUSED_PULL=0 keeps the grouped pull-only
+  // kernel (W <= 32) / k_pull1 (A/B only)
+  static const bool fused_pull = [] {
+    const char* e = std::getenv("P2PG_FUSED_PULL");
+    return !(e && std::strcmp(e, "0") == 0);
+  }();
+  if (fused_pull && st.W <= 64 && st.AW[(p.round & 1) ^ 1] && p.phase < 0) {
+    RoundParams pp = p;
+    pp.store_f = 1;  // the sparse push of this round reads the frontier rows
+    // (K = 0: no picks here, and the relay counters take the run's fanout)
+    if (hp.n_items)
+      hipLaunchKernelGGL((k_pull_hub_partial<false, true>), dim3(grid_tasks(hp.n_items)),
+                         dim3(256), 0, s, g, st, pp, hp);
+    if (st.W <= 32)
+      hipLaunchKernelGGL((k_gossip_fused<false, 0, 3, true>),
+                         dim3(balanced_grid(k_gossip_fused<false, 0, 3, true>, (g.V + 31) >> 5)),
+                         dim3(256), 0, s, g, st, pp);
+    else
+      hipLaunchKernelGGL((k_gossip_fused<false, 0, 3>),
+                         dim3(balanced_grid(k_gossip_fused<false, 0, 3>, (g.V + 31) >> 5)),
+                         dim3(256), 0, s, g, st, pp);
+    if (hp.n_hubs)
+      hipLaunchKernelGGL((k_pull_hub_finalize<true>), dim3(grid_tasks(hp.n_hubs)), dim3(256), 0,
+                         s, g, st, pp, hp);
+    return hipGetLastError();
+  }
   // narrow rows: several peers per wave (the grouped fused kernel without its pushes); the hubs
   // are left to the hub items as in the fused rounds
   if (grouped_enabled() && grouped_pull_enabled() && st.W <= GROUPED_PULL_W_MAX && p.phase < 0) {
@@ -2232,27 +2259,6 @@ hipError_t launch_gossip_pull(const DevGraph& g, const DevState& st, const Round
     if (hp.n_hubs)
       hipLaunchKernelGGL((k_pull_hub_finalize<true>), dim3(grid_tasks(hp.n_hubs)), dim3(256), 0,
                          s, g, st, p, hp);
-    return hipGetLastError();
-  }
-  // wider packed rows: the pull-only mode of the fused kernel (its pipeline crosses task
-  // boundaries); P2PG_FUSED_PULL=0 keeps k_pull1 (A/B only)
-  static const bool fused_pull = [] {
-    const char* e = std::getenv("P2PG_FUSED_PULL");
-    return !(e && std::strcmp(e, "0") == 0);
-  }();
-  if (fused_pull && st.W > GROUPED_PULL_W_MAX && st.W <= 64 && st.AW[(p.round & 1) ^ 1] &&
-      p.phase < 0) {
-    RoundParams pp = p;
-    pp.store_f = 1;  // the sparse push of this round reads the frontier rows
-    if (hp.n_items)
-      hipLaunchKernelGGL((k_pull_hub_partial<false, true>), dim3(grid_tasks(hp.n_items)),
-                         dim3(256), 0, s, g, st, pp, hp);
-    hipLaunchKernelGGL((k_gossip_fused<false, 3, 3>),
-                       dim3(balanced_grid(k_gossip_fused<false, 3, 3>, (g.V + 31) >> 5)), dim3(256),
-                       0, s, g, st, pp);
-    if (hp.n_hubs)
-      hipLaunchKernelGGL((k_pull_hub_finalize<true>), dim3(grid_tasks(hp.n_hubs)), dim3(256), 0,
-                         s, g, st, pp, hp);
     return hipGetLastError();
   }
   return pull_with_hubs<false, true>(g, st, p, hp, s);

@@ -325,6 +325,9 @@ def test_gpu_sparse_push_dedup_matches_golden(name, dedup, monkeypatch):
     # words of bits per hub (long merge groups), fused rounds' hub pushes by atomics, churn
     ("hub", dict(V=1500, m=3, star=1100), 4096, 0, 3),
     ("hub", dict(V=1500, m=3, star=700), 1024, 300_000_000, 5),
+    # 32 < W <= 64 with a ragged last word, churn and fanout 5: the fused kernel's generic-fanout
+    # picks and its pull-only / update+push modes count relays with the run's fanout
+    ("hub", dict(V=1500, m=3, star=700), 3000, 300_000_000, 5),
 ])
 def test_gpu_gossip_push_forms_match_oracle(kind, p, M, thr, fanout, push, monkeypatch):
     """Row atomics, edge stores with fused pull+scatter rounds (k_gossip_fused: every round
