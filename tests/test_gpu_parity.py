@@ -95,6 +95,11 @@ CASES = [
     ("hub", dict(V=1500, m=3, star=1100), "flood", 64, 0),  # pull hub split (deg > 512)
     ("hub", dict(V=1500, m=3, star=1100), "gossip", 128, 0),
     ("hub", dict(V=1500, m=3, star=1100), "flood", 100, 500_000_000),
+    # 32 < W <= 64 floods (the fused kernel's flood mode): ragged last word + churn + hub split,
+    # and full 64-word rows with a wide row (deg > 64)
+    ("hub", dict(V=1500, m=3, star=1100), "flood", 3000, 500_000_000),
+    ("gnp", dict(V=700, k=6.0), "flood", 4096, 0),
+    ("ba", dict(V=150, m=20), "flood", 4000, 300_000_000),
 ]
 
 
