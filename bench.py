@@ -308,8 +308,12 @@ def main():
     if partitioned:
         # one graph, vertex ranges per rank, boundary rows exchanged per round (RCCL all-to-all)
         from p2pnetwork.gpu import PartitionedNetwork, TorchTransport
+        from p2pnetwork.gpu.partition import host_group_for
         src = make_sources(g.V, M, seed=1)
-        net = PartitionedNetwork(g, world, rank, TorchTransport(device=torch.device("cuda", local)), **common)
+        # every rank makes the (collective) gloo group for the count all-gather here
+        hg = host_group_for(None) if args.dist_backend == "nccl" else None
+        net = PartitionedNetwork(g, world, rank,
+                                 TorchTransport(device=torch.device("cuda", local), host_group=hg), **common)
     else:
         # message axis, fixed total work: rank r runs broadcasts [lo, hi) of the M (global ids,
         # so origins and Philox streams are the 1-GPU run's) on its own graph copy.  4096 split

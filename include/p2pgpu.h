@@ -136,7 +136,9 @@ int p2pg_run(p2pg_engine* e, int32_t max_rounds, p2pg_round_stats* per_round,
  * source.  Writes min(cap, count) records; *n_out = count (may exceed cap).
  * A round without first receipts has none (*n_out = 0).  P2PG_ERR_STATE if that round's
  * (or, for the parents, the previous round's) frontier was not kept -- not reachable through
- * p2pg_step / p2pg_run as specified above.                                                 */
+ * p2pg_step / p2pg_run as specified above -- and for the round a snapshot was restored at
+ * (p2pg_restore: the snapshot holds that round's frontier, not the one before it; the rounds
+ * the restored engine runs report their deliveries as usual).                              */
 int p2pg_get_new_deliveries(p2pg_engine* e, int64_t cap, int32_t* peer, int32_t* msg,
                             int32_t* hop, int32_t* parent, int64_t* n_out);
 /* Validation copies: seen [V][W] uint64 (W = ceil(M/64)); hop/parent [V][M] int32 need
@@ -179,6 +181,14 @@ int p2pg_exchange_unpack(p2pg_engine* e, int32_t plane, const void* dev_buf);
 int p2pg_set_exchange_segments(p2pg_engine* e, int32_t nseg, const int64_t* send_counts,
                                const int64_t* recv_counts);
 int p2pg_exchange_pack_live(p2pg_engine* e, int32_t plane, void* dev_buf, int64_t* counts);
+/* Pack inside the round: from now on every p2pg_step / p2pg_step_end packs the live rows of
+ * `plane` into dev_buf (same layout and capacity as pack_live) right after the round's kernels,
+ * and the record counts come back together with the round counters -- one host
+ * synchronisation per round instead of a second drain of the stream for the pack.  A following
+ * p2pg_exchange_pack_live(e, plane, dev_buf, counts) then only returns those counts.  NULL turns
+ * it off.  (Replaces, like pack_live, the cross-host fan-out of NodeConnection.send,
+ * nodeconnection.py:107-160.)                                                              */
+int p2pg_set_exchange_buffer(p2pg_engine* e, int32_t plane, void* dev_buf);
 int p2pg_exchange_unpack_live(p2pg_engine* e, int32_t plane, const void* dev_buf, const int64_t* counts);
 /* A round in two calls, so a vertex-partitioned rank overlaps the exchange of the last round's
  * rows with work: step_begin launches the pull / update of the peers with no ghost neighbour

@@ -66,6 +66,12 @@ struct p2pg_engine {
   int64_t* d_recv_seg = nullptr;
   unsigned long long* d_seg_cnt = nullptr;  // live rows per destination (pack_live)
   unsigned long long* h_seg_cnt = nullptr;  // pinned
+  // p2pg_set_exchange_buffer: every round packs its live rows of this plane into this buffer
+  // right after its kernels, and the counts come back with the round counters (one host
+  // synchronisation per round); pack_live then only hands them over
+  void* auto_buf = nullptr;
+  int32_t auto_plane = -1;
+  int32_t auto_round = -1;           // the round whose records auto_buf / h_seg_cnt hold
   bool begun = false;                 // p2pg_step_begin ran this round's phase 0
   bool last_push_e = false;    // gossip: pushes of the previous round went to E (dense)
   double e_thresh = 0.06;      // store-mode when active words >= thresh * active rows * W;
@@ -238,6 +244,8 @@ void free_graph(p2pg_engine* e) {
   dfree(e->d_seg_cnt);
   if (e->h_seg_cnt) (void)hipHostFree(e->h_seg_cnt);
   e->h_seg_cnt = nullptr;
+  e->auto_buf = nullptr;
+  e->auto_plane = e->auto_round = -1;
   e->send_seg.clear();
   e->recv_seg.clear();
   e->h_gid.clear();
@@ -711,6 +719,7 @@ int p2pg_reset(p2pg_engine* e) {
   e->round = 0;
   e->done = false;
   e->begun = false;
+  e->auto_round = -1;
   e->frontier_kept = true;
   e->frontier_kept_prev = true;
   e->last_push_e = false;
@@ -912,6 +921,22 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
       return rc;
     e->last_push_e = use_e;
   }
+  if (e->auto_buf && e->d_seg_cnt) {
+    // partitioned ranks: pack this round's live boundary rows now, so the one synchronisation
+    // below (the round counters) also covers the pack and its counts -- no second drain of the
+    // stream before the records leave (p2pg_set_exchange_buffer)
+    const bool fwd = e->auto_plane == 0;
+    const int nseg = (int)e->send_seg.size() - 1;
+    HIPCHK(e, hipMemsetAsync(e->d_seg_cnt, 0, sizeof(unsigned long long) * P2PG_MAX_RANKS, e->stream));
+    hipError_t r = launch_pack_live(s, e->auto_plane, e->round, fwd ? e->d_send : e->d_recv,
+                                    fwd ? e->n_send : e->n_recv, fwd ? e->d_send_seg : e->d_recv_seg,
+                                    nseg, e->d_seg_cnt, (int64_t*)e->auto_buf, e->stream);
+    if (r == hipSuccess)
+      r = hipMemcpyAsync(e->h_seg_cnt, e->d_seg_cnt, sizeof(unsigned long long) * nseg,
+                         hipMemcpyDeviceToHost, e->stream);
+    if (r != hipSuccess) return fail(e, P2PG_ERR_HIP, std::string("step (exchange pack): ") + hipGetErrorString(r));
+    e->auto_round = e->round;
+  }
   if ((rc = read_stats())) return rc;
   if ((rc = check_scatter_list(e, e->h_stats[STAT_COUNT]))) return rc;
 #ifdef P2PG_PROF
@@ -989,8 +1014,12 @@ int p2pg_get_new_deliveries(p2pg_engine* e, int64_t cap, int32_t* peer, int32_t*
     *n_out = 0;
     return P2PG_OK;
   }
-  if (!e->frontier_kept || !e->frontier_kept_prev)
-    return fail(e, P2PG_ERR_STATE, "get_new_deliveries: the last rounds' frontiers were not kept");
+  if (!e->frontier_kept)
+    return fail(e, P2PG_ERR_STATE, "get_new_deliveries: the last round's frontier was not kept");
+  if (!e->frontier_kept_prev)
+    return fail(e, P2PG_ERR_STATE, "get_new_deliveries: the parents need the frontier of the round "
+                                   "before, which was not kept (a fused round inside p2pg_run, or "
+                                   "the round a snapshot was restored at)");
   HIPCHK(e, hipSetDevice(e->cfg.device));
   // the most recent round is e->round - 1; its frontier is F[(round-1)&1]
   RoundParams p = params(e);
@@ -1153,6 +1182,25 @@ int p2pg_set_exchange_segments(p2pg_engine* e, int32_t nseg, const int64_t* send
   return P2PG_OK;
 }
 
+int p2pg_set_exchange_buffer(p2pg_engine* e, int32_t plane, void* dev_buf) {
+  if (!e) return P2PG_ERR_ARG;
+  if (!dev_buf) {
+    e->auto_buf = nullptr;
+    e->auto_plane = -1;
+    e->auto_round = -1;
+    return P2PG_OK;
+  }
+  if (plane != 0 && plane != 1) return fail(e, P2PG_ERR_ARG, "set_exchange_buffer: plane 0 or 1");
+  if (!e->d_seg_cnt) return fail(e, P2PG_ERR_STATE, "set_exchange_buffer: set_exchange_segments first");
+  if (plane == 1 && e->cfg.mode != P2PG_MODE_GOSSIP)
+    return fail(e, P2PG_ERR_ARG, "set_exchange_buffer: plane 1 is for gossip pushes");
+  if (e->begun) return fail(e, P2PG_ERR_STATE, "set_exchange_buffer: a round has begun (step_begin)");
+  e->auto_buf = dev_buf;
+  e->auto_plane = plane;
+  e->auto_round = -1;
+  return P2PG_OK;
+}
+
 int p2pg_exchange_pack_live(p2pg_engine* e, int32_t plane, void* dev_buf, int64_t* counts) {
   if (!e || !e->have_state || e->round == 0 || (plane != 0 && plane != 1) || !dev_buf || !counts)
     return fail(e, P2PG_ERR_STATE, "exchange_pack_live: need a completed round, plane 0 or 1, buffers");
@@ -1160,8 +1208,14 @@ int p2pg_exchange_pack_live(p2pg_engine* e, int32_t plane, void* dev_buf, int64_
   if (e->begun) return fail(e, P2PG_ERR_STATE, "exchange_pack_live: the next round has begun");
   if (plane == 1 && e->cfg.mode != P2PG_MODE_GOSSIP)
     return fail(e, P2PG_ERR_ARG, "exchange_pack_live: plane 1 is for gossip pushes");
-  HIPCHK(e, hipSetDevice(e->cfg.device));
   const int nseg = (int)e->send_seg.size() - 1;
+  if (dev_buf == e->auto_buf && plane == e->auto_plane && e->auto_round == e->round - 1) {
+    // packed by the round itself (p2pg_set_exchange_buffer), counts read with its counters
+    for (int q = 0; q < nseg; ++q) counts[q] = (int64_t)e->h_seg_cnt[q];
+    e->auto_round = -1;  // handed over once
+    return P2PG_OK;
+  }
+  HIPCHK(e, hipSetDevice(e->cfg.device));
   // plane 0 moves frontier rows owner -> ghost (send list); plane 1 pushes ghost -> owner
   const bool fwd = plane == 0;
   const int32_t* ids = fwd ? e->d_send : e->d_recv;
@@ -1365,7 +1419,7 @@ int p2pg_update_edges(p2pg_engine* e, int64_t n_add, const int32_t* add, int64_t
 namespace {
 
 constexpr uint64_t SNAP_MAGIC = 0x50414E5347503250ull;  // "P2PGSNAP"
-constexpr uint32_t SNAP_VERSION = 1;
+constexpr uint32_t SNAP_VERSION = 2;  // 2: + last_new
 
 struct SnapHeader {
   uint64_t magic;
@@ -1375,6 +1429,7 @@ struct SnapHeader {
   uint32_t flags, churn_threshold, msg_id_base, done;
   uint32_t consume_next, has_next;
   uint64_t gossip_seed, churn_seed, graph_hash, src_hash, total_relays, prev_aw, prev_av;
+  uint64_t last_new;  // first receipts of the last round (deliveries, decay-phase push dedup)
 };
 
 uint64_t fnv1a(uint64_t h, const void* data, size_t n) {
@@ -1480,6 +1535,7 @@ int p2pg_snapshot(p2pg_engine* e, void* buf, int64_t cap) {
   h.total_relays = e->total_relays;
   h.prev_aw = e->prev_aw;
   h.prev_av = e->prev_av;
+  h.last_new = e->last_new;
   char* out = (char*)buf;
   std::memcpy(out, &h, sizeof(h));
   size_t off = sizeof(h);
@@ -1538,6 +1594,11 @@ int p2pg_restore(p2pg_engine* e, const void* buf, int64_t size) {
   e->total_relays = h.total_relays;
   e->prev_aw = h.prev_aw;
   e->prev_av = h.prev_av;
+  e->last_new = h.last_new;
+  // the snapshot holds the last round's frontier, not the one before it, so that round's
+  // delivery parents cannot be found (round 0's are -1): deliveries refuse it, as documented
+  e->frontier_kept = true;
+  e->frontier_kept_prev = h.round <= 1;
   e->prev2_aw = e->prev2_av = e->prev2_new = 0;  // no growth history: no update+push prediction
   const char* in = (const char*)buf;
   size_t off = sizeof(h);

@@ -98,6 +98,7 @@ SIGNATURES = {
     "p2pg_set_exchange_segments": (ctypes.c_int, [_P, _I32, _P, _P]),
     "p2pg_exchange_pack_live": (ctypes.c_int, [_P, _I32, _P, _P]),
     "p2pg_exchange_unpack_live": (ctypes.c_int, [_P, _I32, _P, _P]),
+    "p2pg_set_exchange_buffer": (ctypes.c_int, [_P, _I32, _P]),
     "p2pg_step_begin": (ctypes.c_int, [_P]),
     "p2pg_step_end": (ctypes.c_int, [_P, ctypes.POINTER(RoundStatsC)]),
     "p2pg_set_stream": (ctypes.c_int, [_P, _P]),

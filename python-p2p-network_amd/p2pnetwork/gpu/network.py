@@ -342,6 +342,12 @@ class GraphNetwork:
                                                        _lib.ptr(counts)))
         return counts
 
+    def set_exchange_buffer(self, plane, buf):
+        """Pack the live rows of ``plane`` into device buffer ``buf`` inside every round, their
+        counts read back with the round counters (p2pg_set_exchange_buffer); ``None`` = off."""
+        self._check(_lib.lib().p2pg_set_exchange_buffer(
+            self._h, int(plane), ctypes.c_void_p(buf.data_ptr()) if buf is not None else None))
+
     def exchange_unpack_live(self, plane, buf, counts):
         c = np.ascontiguousarray(counts, dtype=np.int64)
         self._check(_lib.lib().p2pg_exchange_unpack_live(self._h, int(plane), ctypes.c_void_p(buf.data_ptr()),

@@ -96,6 +96,15 @@ class VertexPartition:
         return np.where(held, pos, self.dummy).astype(np.int32)
 
 
+def host_group_for(group=None):
+    """A gloo group with the ranks of ``group`` (None = the default group), for the host-side
+    count all-gather next to an RCCL group.  Collective over the default group: call it on
+    every rank of the job."""
+    import torch.distributed as dist
+    ranks = list(range(dist.get_world_size())) if group is None else dist.get_process_group_ranks(group)
+    return dist.new_group(ranks=ranks, backend="gloo")
+
+
 class TorchTransport:
     """The two collectives of a partitioned round over a torch.distributed process group.
     With the nccl backend (RCCL on ROCm) records move device-to-device over xGMI; with gloo
@@ -110,7 +119,7 @@ class TorchTransport:
     * ``engine_stream()``: the stream the rank's engine should launch on (device runs), so
       that the receives can be ordered before the unpack by a stream wait, not a host sync."""
 
-    def __init__(self, device=None, group=None):
+    def __init__(self, device=None, group=None, host_group=None):
         import torch
         import torch.distributed as dist
         self.torch, self.dist, self.group = torch, dist, group
@@ -118,11 +127,19 @@ class TorchTransport:
         self.device = device
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
-        # counts travel host-side; with RCCL that needs a gloo group next to the nccl one
-        # (a collective call: every rank constructs its transport at the same point)
-        self.host_group = group if self.backend == "gloo" else dist.new_group(
-            ranks=list(range(self.world)) if group is None else dist.get_process_group_ranks(group),
-            backend="gloo")
+        # counts travel host-side; with RCCL that needs a gloo group next to the nccl one.
+        # Pass it in (host_group_for) when `group` is a subgroup: creating a group is collective
+        # over the DEFAULT group, so every rank of the job must make that call, not only the
+        # ranks that build a transport.
+        if self.backend == "gloo":
+            self.host_group = group
+        elif host_group is not None:
+            self.host_group = host_group
+        elif group is None:
+            self.host_group = host_group_for(None)
+        else:
+            raise ValueError("TorchTransport over an RCCL subgroup: pass host_group="
+                             "host_group_for(group), created by every rank of the job")
         self.rows_total = 0  # boundary rows offered / actually sent (exchange volume)
         self.rows_sent = 0
 
@@ -186,6 +203,7 @@ class PartitionedNetwork:
         self.deg = graph.degree().astype(np.int32)  # global degrees (round-0 counters); the
         # global graph itself is not kept: the engine holds only the rank-local CSR
         self.mode, self.fanout = mode, fanout
+        self._plane = 0 if mode == "flood" else 1  # rows that travel: frontier / ghost pushes
         self.overlap = overlap
         self.part = VertexPartition(graph, world, rank)
         make = engine_factory or GraphNetwork
@@ -222,6 +240,10 @@ class PartitionedNetwork:
         W = (self.M + 63) // 64
         rows = max(len(self.part.send_local), len(self.part.recv_local), 1)
         self._bufs = (self.net.alloc_exchange(rows * (1 + W)), self.net.alloc_exchange(rows * (1 + W)))
+        if self.world > 1 and hasattr(self.net, "set_exchange_buffer"):
+            # the round packs its live rows itself: their counts arrive with the round counters,
+            # so exchange_pack_live below costs no second stream drain before the sends
+            self.net.set_exchange_buffer(self._plane, self._bufs[0])
 
     def reset(self):
         self.net.reset()
@@ -266,7 +288,7 @@ class PartitionedNetwork:
             W = (self.M + 63) // 64
             R = 1 + W
             p = self.part
-            plane = 0 if self.mode == "flood" else 1
+            plane = self._plane
             # plane 0: frontier rows owner -> ghost holders; plane 1: pushes ghost -> owner
             send_rows, recv_rows = (p.send_counts, p.recv_counts) if plane == 0 else (p.recv_counts, p.send_counts)
             send_off = np.concatenate([[0], np.cumsum(send_rows)]).astype(np.int64)

@@ -65,3 +65,25 @@ def test_bench_gpus2_spawns_two_ranks():
     assert j2["n_gpus"] == 2
     assert j2["relays_per_step"] == C2_RELAYS
     assert "x2" in j2["config"]["parallelism"]
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+def test_bench_c5_partitioned_8_ranks_gloo():
+    """Config 5's vertex-partitioned job at 8 ranks (gloo, all on cuda:0 of the one-GPU box) at
+    2M peers, W = 64, churn 0.05: the JSON line reports n_gpus 8 and the same relays per step as
+    the unpartitioned 1-GPU run of the same size (records of 1 + 64 int64 through 8 list segments,
+    interior peers overlapping the exchange)."""
+    common = ["--workload", "c5", "--peers", "2000000", "--steps", "1", "--warmup", "0",
+              "--no-cpu-baseline"]
+    one = _bench(["--gpus", "1", *common], _env(), timeout=300)
+    assert one.returncode == 0, one.stderr[-4000:]
+    j1 = _json_line(one.stdout)
+    eight = _bench(["--gpus", "8", "--dist-backend", "gloo", *common], _env(), timeout=600)
+    assert eight.returncode == 0, eight.stderr[-4000:]
+    j8 = _json_line(eight.stdout)
+    assert j8["n_gpus"] == 8
+    assert "vertex partition x8" in j8["config"]["parallelism"]
+    assert j8["relays_per_step"] == j1["relays_per_step"]
+    assert j8["config"]["rounds"] == j1["config"]["rounds"]
+    assert 0.0 < j8["exchange_live_row_frac"] <= 1.0

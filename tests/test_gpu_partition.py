@@ -3,6 +3,7 @@ partition entry points: global ids, exchange lists, pack/unpack kernels) on cuda
 run as threads of one process and a thread transport stands in for the all-to-all.  The union
 of the owned results must equal the single-engine run and the oracle bit for bit."""
 import threading
+from types import SimpleNamespace
 
 import numpy as np
 import pytest
@@ -152,3 +153,87 @@ def test_partitioned_gossip_small_matches_numpy_oracle():
     np.testing.assert_array_equal(bits, ora.hop >= 0)
     np.testing.assert_array_equal(trim_zeros([r.relays for r in res[0][0]]),
                                   trim_zeros([r["relays"] for r in ora.rounds]))
+
+
+# --- the multi-GPU forms at their real widths (W = 64, 8 ranks), on the one GPU ---------------
+# config 5's job (bench.py --workload c5 --gpus 8) packs records of 1 + 64 int64 per live row
+# across 8 list segments with the next round's interior peers overlapping the exchange; here that
+# combination runs with real engines (8 thread-ranks on cuda:0) at 1M peers before any 8-GPU job
+# does, against one engine and against the C oracle (nodeconnection.py:107-160 is the fan-out it
+# replaces, node.py:106-120 the relay).
+
+def _c5_like():
+    from p2pnetwork.gpu import PeerGraph
+    from p2pnetwork.gpu.network import churn_threshold
+    return PeerGraph.watts_strogatz(1_000_000, 8, 0.1, seed=5), churn_threshold(0.05)
+
+
+def _round_keys(rounds):
+    keys = ("new_deliveries", "relays", "active_vertices", "active_words", "wedges", "deg_active",
+            "scatter_words")
+    return {k: trim_zeros([getattr(r, k) for r in rounds]) for k in keys}
+
+
+def _assert_same_rounds(got, want):
+    a, b = _round_keys(got), _round_keys(want)
+    for k in a:
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+
+
+def test_partitioned_8_ranks_full_width_flood_churn():
+    """8 ranks, WS k=8 beta=0.1 at 1M peers, 4096 floods (W = 64), churn 0.05, overlap on: the
+    assembled seen plane and every global per-round counter == one engine; words 0 and 63 ==
+    64-broadcast partitioned runs whose hop / parent planes == the C oracle's bit for bit."""
+    from p2pnetwork.gpu import GraphNetwork, make_sources
+    g, thr = _c5_like()
+    M, world = 4096, 8
+    src = make_sources(g.V, M, seed=1)
+    kw = dict(mode="flood", churn_threshold_value=thr, churn_seed=0xC0FFEE)
+    res = run_partitioned(g, world, src, overlap=True, **kw)
+    with GraphNetwork(g, **kw) as one:
+        one.broadcast(src)
+        rounds1 = one.run()
+        seen1 = one.seen_plane()
+    seen = assemble(res, g.V, M // 64)
+    np.testing.assert_array_equal(seen, seen1)
+    for rounds, *_ in res:
+        _assert_same_rounds(rounds, rounds1)
+    for w in (0, 63):
+        s = src[64 * w:64 * (w + 1)]
+        part = run_partitioned(g, world, s, overlap=True, record=True, **kw)
+        np.testing.assert_array_equal(assemble(part, g.V, 1)[:, 0], seen[:, w], err_msg=f"word {w}")
+        hop = np.full((g.V, 64), -1, np.int32)
+        par = np.full((g.V, 64), -1, np.int32)
+        for _, _, _, (gids, h, p) in part:
+            hop[gids], par[gids] = h, p
+        ora = coracle.run(g.rowptr, g.colidx, s, "flood", 3, 0, 0, thr, 0xC0FFEE, record=True)
+        np.testing.assert_array_equal(hop, ora.hop, err_msg=f"word {w} hop")
+        np.testing.assert_array_equal(par, ora.parent, err_msg=f"word {w} parent")
+        _assert_same_rounds(part[0][0], [SimpleNamespace(**r) for r in ora.rounds])
+
+
+def test_partitioned_8_ranks_full_width_gossip():
+    """Gossip (k = 3, churn 0.05) over 8 ranks at W = 64 on a 1M-peer BA graph (hubs at the low
+    ids, on rank 0): the assembled seen plane and the global per-round counters == one engine;
+    words 0 and 63 == the C oracle's delivered sets (their broadcasts run alone, with their global
+    message ids)."""
+    from p2pnetwork.gpu import GraphNetwork, PeerGraph, make_sources
+    from p2pnetwork.gpu.network import churn_threshold
+    g = PeerGraph.barabasi_albert(1_000_000, 4, seed=11)
+    thr = churn_threshold(0.05)
+    M, world = 4096, 8
+    src = make_sources(g.V, M, seed=1)
+    kw = dict(mode="gossip", fanout=3, gossip_seed=0x5EED, churn_threshold_value=thr, churn_seed=0xC0FFEE)
+    res = run_partitioned(g, world, src, overlap=True, **kw)
+    with GraphNetwork(g, **kw) as one:
+        one.broadcast(src)
+        rounds1 = one.run()
+        seen1 = one.seen_plane()
+    seen = assemble(res, g.V, M // 64)
+    np.testing.assert_array_equal(seen, seen1)
+    for rounds, *_ in res:
+        _assert_same_rounds(rounds, rounds1)
+    for w in (0, 63):
+        ora = coracle.run(g.rowptr, g.colidx, src[64 * w:64 * (w + 1)], "gossip", 3, 0x5EED, 64 * w, thr,
+                          0xC0FFEE, record=False, want_seen=True)
+        np.testing.assert_array_equal(seen[:, w], ora.seen[:, 0], err_msg=f"word {w}")

@@ -1,6 +1,6 @@
 """HBM traffic per launch of each relay kernel class from rocprofv3 PMC passes, calibrated.
 
-    python tools/pmc_traffic.py CAL_DIR RUN_DIR WORKLOAD OUT_JSON
+    python tools/pmc_traffic.py CAL_DIR RUN_DIR WORKLOAD OUT_JSON [BUILD_SHA]
 
 CAL_DIR: FETCH_SIZE / WRITE_SIZE passes over tools/microbench/atomics (known payloads:
 seq_read, row_read, row_store of 5.12 GB each) -> bytes-per-counter-unit for 16 B/lane streams,
@@ -49,9 +49,19 @@ def calib(d):
 def cls(name):
     """rocprof kernel name -> bench.py timer class (include/p2pgpu.h P2PG_KCLASS_N)."""
     tmpl = name.split("<", 1)[1].split(">(")[0] if "<" in name else ""
-    if "k_gossip_fused" in name and tmpl.count(",") >= 2 and tmpl.rsplit(",", 1)[1].strip() in ("1", "2"):
-        return "gossip_scatter_store"  # push-only / update+push modes (timed with the store pushes)
-    if "k_gossip_fused" in name or "k_wide_zero" in name or "k_wide_push" in name:
+    targs = [t.strip() for t in tmpl.split(",")] if tmpl else []
+    if "k_gossip_fused_grouped" in name:
+        # <CHURN, K, LW, PO, PL>: push-only = the store pushes, pull-only = the last dense pull
+        po = len(targs) > 3 and targs[3] == "true"
+        pl = len(targs) > 4 and targs[4] == "true"
+        return "gossip_scatter_store" if po else "gossip_pull" if pl else "gossip_fused"
+    if "k_gossip_fused" in name:
+        # <CHURN, K, MODE, HALF>: MODE 1 push-only / 2 update+push (timed with the store pushes),
+        # 3 pull-only (timed as the last dense round's pull), 0 the fused round
+        mode = targs[2] if len(targs) > 2 else "0"
+        return {"1": "gossip_scatter_store", "2": "gossip_scatter_store",
+                "3": "gossip_pull"}.get(mode, "gossip_fused")
+    if "k_wide_zero" in name or "k_wide_push" in name:
         return "gossip_fused"  # (the hub pushes ride in the fused rounds' timed launch group)
     if any(x in name for x in ("k_sparse_words", "k_chunk_scan", "k_sparse_push", "k_touched_bits")):
         return "gossip_scatter_atomic"
@@ -87,7 +97,8 @@ def main():
                                          "k_touched_bits"))
         a["n"] += 1 if ("FETCH_SIZE" in c and not helper) else 0
         a["ns"] += c["ns"] if "FETCH_SIZE" in c else 0
-    res = {"workload": wl, "calibration": cal, "source": run_dir, "kernels": {}}
+    res = {"workload": wl, "build_sha": sys.argv[5] if len(sys.argv) > 5 else None,
+           "calibration": cal, "source": run_dir, "kernels": {}}
     # the scatter and both consume kernels share class names with bench.py's timers
     for k, a in agg.items():
         n = max(a["n"], 1)
