@@ -166,6 +166,15 @@ int p2pg_kernel_times(p2pg_engine* e, double ms[P2PG_KCLASS_N], int64_t launches
  * memory of n x W uint64 words.  Replaces the cross-host TCP fan-out of
  * NodeConnection.send (nodeconnection.py:107-160).                                      */
 int p2pg_set_global_ids(p2pg_engine* e, const int32_t* gid);
+/* Partitioned gossip, for hop / parent records and the delivery stream: a first receipt's
+ * parent is the lowest-id neighbour whose Philox picks chose the receiver (node.py:334-338's
+ * sender), and a GHOST neighbour's picks depend on its global degree and the
+ * receiver's place in its global adjacency, which the rank-local graph does not hold:
+ * ghost_deg[local] = global degree of each ghost (any value for owned peers), slot_pos[j] for
+ * every local slot j = position of the slot's row owner in the neighbour's global ascending
+ * adjacency when the neighbour is a ghost, else -1.  The ghosts' frontier rows must then also
+ * travel each round (plane 0).  NULL, NULL removes them.                                   */
+int p2pg_set_ghost_senders(p2pg_engine* e, const int32_t* ghost_deg, const int32_t* slot_pos);
 int p2pg_set_exchange(p2pg_engine* e, int64_t n_send, const int32_t* send_local, int64_t n_recv,
                       const int32_t* recv_local);
 int p2pg_exchange_pack(p2pg_engine* e, int32_t plane, void* dev_buf);

@@ -57,6 +57,8 @@ struct p2pg_engine {
   // vertex-partitioned runs
   int32_t* d_gid = nullptr;
   std::vector<int32_t> h_gid;
+  int32_t* d_gdeg = nullptr;          // ghost senders' global degrees (p2pg_set_ghost_senders)
+  int32_t* d_gpos = nullptr;          // per local slot: position in the ghost neighbour's row
   int32_t* d_send = nullptr;
   int32_t* d_recv = nullptr;
   int64_t n_send = 0, n_recv = 0;
@@ -236,6 +238,8 @@ void free_graph(p2pg_engine* e) {
   dfree(e->d_hub_begin);
   dfree(e->d_partial);
   dfree(e->d_gid);
+  dfree(e->d_gdeg);
+  dfree(e->d_gpos);
   dfree(e->d_send);
   dfree(e->d_recv);
   dfree(e->d_border);
@@ -275,14 +279,16 @@ RoundParams params(const p2pg_engine* e) {
 }
 
 DevGraph graph(const p2pg_engine* e) {
-  return DevGraph{e->d_rowptr, e->d_colidx, e->d_rev, e->d_H, e->d_gid, nullptr, e->V};
+  return DevGraph{e->d_rowptr, e->d_colidx, e->d_rev, e->d_H, e->d_gid, nullptr, e->V,
+                  e->d_gdeg, e->d_gpos};
 }
 
 // The graph round r's arrivals travelled on: the pre-update graph (with its removed slots) for
 // the round right after a topology update, else the current one.
 DevGraph graph_for_arrivals(const p2pg_engine* e, int32_t r) {
   if (r == e->arr_round && e->d_rowptr_arr)
-    return DevGraph{e->d_rowptr_arr, e->d_colidx_arr, nullptr, nullptr, e->d_gid, e->d_gone, e->V};
+    return DevGraph{e->d_rowptr_arr, e->d_colidx_arr, nullptr, nullptr, e->d_gid, e->d_gone, e->V,
+                    nullptr, nullptr};
   return graph(e);
 }
 
@@ -1112,6 +1118,27 @@ int p2pg_set_global_ids(p2pg_engine* e, const int32_t* gid) {
   e->h_gid.assign(gid, gid + e->V);
   HIPCHK(e, hipMalloc((void**)&e->d_gid, sizeof(int32_t) * e->V));
   HIPCHK(e, hipMemcpy(e->d_gid, gid, sizeof(int32_t) * e->V, hipMemcpyHostToDevice));
+  return P2PG_OK;
+}
+
+int p2pg_set_ghost_senders(p2pg_engine* e, const int32_t* ghost_deg, const int32_t* slot_pos) {
+  if (!e || !e->d_rowptr) return fail(e, P2PG_ERR_STATE, "set_ghost_senders: load a graph first");
+  HIPCHK(e, hipSetDevice(e->cfg.device));
+  dfree(e->d_gdeg);
+  dfree(e->d_gpos);
+  if (!ghost_deg && !slot_pos) return P2PG_OK;
+  if (!ghost_deg || !slot_pos) return fail(e, P2PG_ERR_ARG, "set_ghost_senders: need both arrays");
+  for (int64_t v = 0; v < e->V; ++v)
+    for (int64_t j = e->h_rowptr[v]; j < e->h_rowptr[v + 1]; ++j) {
+      const int32_t u = e->h_colidx[j];
+      if (slot_pos[j] < -1 || (slot_pos[j] >= 0 && slot_pos[j] >= ghost_deg[u]))
+        return fail(e, P2PG_ERR_ARG, "set_ghost_senders: slot position outside the ghost's row");
+    }
+  HIPCHK(e, hipMalloc((void**)&e->d_gdeg, sizeof(int32_t) * (size_t)e->V));
+  HIPCHK(e, hipMalloc((void**)&e->d_gpos, sizeof(int32_t) * (size_t)(e->nnz ? e->nnz : 1)));
+  HIPCHK(e, hipMemcpy(e->d_gdeg, ghost_deg, sizeof(int32_t) * (size_t)e->V, hipMemcpyHostToDevice));
+  if (e->nnz)
+    HIPCHK(e, hipMemcpy(e->d_gpos, slot_pos, sizeof(int32_t) * (size_t)e->nnz, hipMemcpyHostToDevice));
   return P2PG_OK;
 }
 

@@ -87,6 +87,7 @@ __global__ __launch_bounds__(256, P2PG_GROUPED_WAVES) void k_gossip_fused_groupe
   // never partitioned and never on a pre-update graph (the engine's dense rounds): the id
   // translation and lost-slot tests fold away
   g.gid = nullptr;
+  g.gdeg = g.gpos = nullptr;
   g.gone = nullptr;
   constexpr int WP = Lds::WP;
   constexpr int TS = Lds::TS;

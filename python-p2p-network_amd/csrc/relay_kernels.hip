@@ -1503,6 +1503,7 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
   // so the id translation and lost-slot tests fold away (fewer live scalar registers)
   g.gid = nullptr;
   g.gone = nullptr;
+  g.gdeg = g.gpos = nullptr;
   __shared__ ScatterLds lds[WPB];
   const int lane = threadIdx.x & 63;
   const int wib = wave_in_block();
@@ -1927,12 +1928,18 @@ __device__ int32_t find_parent(const DevGraph& g, const DevState& st, const Roun
       continue;
     if (p.mode == 1) {
       const int64_t vb = g.rowptr[v];
-      const int64_t dv = g.rowptr[v + 1] - vb;
+      // a ghost sender (partitioned runs): its global degree and u's place in its global row
+      const bool ghost = g.gpos && g.gpos[e] >= 0;
+      const int64_t dv = ghost ? (int64_t)g.gdeg[v] : g.rowptr[v + 1] - vb;
       if (dv > p.fanout) {
         int64_t lo = 0, hi = dv;  // position of u in v's ascending list
-        while (lo < hi) {
-          const int64_t mid = (lo + hi) >> 1;
-          if (g.colidx[vb + mid] < u) lo = mid + 1; else hi = mid;
+        if (ghost) {
+          lo = g.gpos[e];
+        } else {
+          while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (g.colidx[vb + mid] < u) lo = mid + 1; else hi = mid;
+          }
         }
         uint32_t pk[16];
         gossip_picks((uint32_t)(p.round - 1), gidx(g, v), p.msg_base + (uint32_t)m,

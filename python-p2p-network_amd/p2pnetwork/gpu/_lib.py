@@ -93,6 +93,7 @@ SIGNATURES = {
     "p2pg_kernel_times": (ctypes.c_int, [_P, _P, _P]),
     "p2pg_set_global_ids": (ctypes.c_int, [_P, _P]),
     "p2pg_set_exchange": (ctypes.c_int, [_P, _I64, _P, _I64, _P]),
+    "p2pg_set_ghost_senders": (ctypes.c_int, [_P, _P, _P]),
     "p2pg_exchange_pack": (ctypes.c_int, [_P, _I32, _P]),
     "p2pg_exchange_unpack": (ctypes.c_int, [_P, _I32, _P]),
     "p2pg_set_exchange_segments": (ctypes.c_int, [_P, _I32, _P, _P]),

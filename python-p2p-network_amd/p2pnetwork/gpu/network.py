@@ -262,6 +262,14 @@ class GraphNetwork:
         return (self.callback is not None
                 or type(self).node_message_batch is not GraphNetwork.node_message_batch)
 
+    def deliveries_count(self):
+        """Number of first-receipt records the last round's delivery stream holds."""
+        n = ctypes.c_int64()
+        z = np.zeros(1, dtype=np.int32)
+        self._check(_lib.lib().p2pg_get_new_deliveries(self._h, 0, _lib.ptr(z), _lib.ptr(z), _lib.ptr(z),
+                                                        _lib.ptr(z), ctypes.byref(n)))
+        return int(n.value)
+
     def deliveries(self, cap=None):
         """First receipts of the most recent round as (peer, msg, hop, parent) arrays."""
         if cap is None:
@@ -321,6 +329,14 @@ class GraphNetwork:
     def set_global_ids(self, gid):
         self._gid = np.ascontiguousarray(gid, dtype=np.int32)
         self._check(_lib.lib().p2pg_set_global_ids(self._h, _lib.ptr(self._gid)))
+
+    def set_ghost_senders(self, ghost_deg, slot_pos):
+        """Partitioned gossip records / deliveries: the ghosts' global degrees and, per local
+        slot, the row owner's position in its ghost neighbour's global adjacency (-1 = local
+        neighbour) -- p2pg_set_ghost_senders."""
+        self._gdeg = np.ascontiguousarray(ghost_deg, dtype=np.int32)
+        self._gpos = np.ascontiguousarray(slot_pos, dtype=np.int32)
+        self._check(_lib.lib().p2pg_set_ghost_senders(self._h, _lib.ptr(self._gdeg), _lib.ptr(self._gpos)))
 
     def set_exchange(self, send_local, recv_local):
         s = np.ascontiguousarray(send_local, dtype=np.int32)

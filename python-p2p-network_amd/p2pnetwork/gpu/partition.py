@@ -81,6 +81,34 @@ class VertexPartition:
         self.send_counts = counts
         self.send_local = np.searchsorted(self.gid, send).astype(np.int32)
 
+    def ghost_senders(self, graph):
+        """(ghost_deg [V_local], slot_pos [local slots]) for p2pg_set_ghost_senders: a ghost's
+        global degree, and for every local slot whose neighbour is a ghost the row owner's
+        position in that ghost's global ascending adjacency (-1 for a local neighbour) -- what
+        replaying a remote sender's gossip picks needs (hop / parent records, deliveries)."""
+        rp, ci = graph.rowptr, graph.colidx
+        V = graph.V
+        gid = self.gid[:-1].astype(np.int64)            # without the dummy sink
+        ghost_deg = np.zeros(self.V_local, dtype=np.int32)
+        ghost_deg[:-1] = (rp[gid + 1] - rp[gid]).astype(np.int32)
+        nb = gid[self.colidx.astype(np.int64)]          # global neighbour of each local slot
+        rows = np.repeat(gid, np.diff(self.rowptr)[:-1])  # row owner of each slot (dummy: none)
+        remote = (nb < self.lo) | (nb >= self.hi)
+        pos = np.full(len(nb), -1, dtype=np.int32)
+        if remote.any():
+            us, vs = nb[remote], rows[remote]
+            # the ghosts' global rows, concatenated in ascending (ghost, neighbour) key order
+            ghosts = np.unique(us)
+            starts, ends = rp[ghosts], rp[ghosts + 1]
+            lens = ends - starts
+            off = np.concatenate([[0], np.cumsum(lens)])
+            idx = np.repeat(starts - off[:-1], lens) + np.arange(off[-1])
+            keys = np.repeat(ghosts, lens) * V + ci[idx].astype(np.int64)
+            at = np.searchsorted(keys, us * V + vs)
+            assert np.array_equal(keys[at], us * V + vs), "asymmetric adjacency"
+            pos[remote] = (at - off[np.searchsorted(ghosts, us)]).astype(np.int32)
+        return ghost_deg, pos
+
     def owner(self, g):
         return (np.searchsorted(self.bounds, np.asarray(g), side="right") - 1).astype(np.int64)
 
@@ -193,13 +221,15 @@ class PartitionedNetwork:
 
     def __init__(self, graph, world, rank, transport, mode="flood", fanout=3, gossip_seed=0x5EED,
                  churn_threshold_value=0, churn_seed=0xC0FFEE, record=False, timing=False,
-                 device=0, engine_factory=None, overlap=True):
+                 device=0, engine_factory=None, overlap=True, deliveries=False):
         if not 1 <= world <= MAX_RANKS:
             raise ValueError(f"vertex partition over {world} ranks: the exchange supports 1..{MAX_RANKS}")
-        if record and mode == "gossip" and world > 1:
-            # a gossip parent check needs the REMOTE sender's degree and adjacency order
-            raise NotImplementedError("record=True for partitioned gossip: record on one GPU")
         self.world, self.rank, self.transport = world, rank, transport
+        # partitioned gossip with hop / parent records or the per-round delivery stream: a
+        # parent is the lowest-id neighbour whose picks chose the receiver (node.py:334-338's
+        # sender), and for a ghost sender the rank needs its frontier rows (plane 0 travels
+        # too, owner -> ghost holders) and its global degree / adjacency order
+        self._senders = mode == "gossip" and world > 1 and (record or deliveries)
         self.deg = graph.degree().astype(np.int32)  # global degrees (round-0 counters); the
         # global graph itself is not kept: the engine holds only the rank-local CSR
         self.mode, self.fanout = mode, fanout
@@ -221,6 +251,8 @@ class PartitionedNetwork:
         self.net.set_global_ids(self.part.gid)
         self.net.set_exchange(self.part.send_local, self.part.recv_local)
         self.net.set_exchange_segments(self.part.send_counts, self.part.recv_counts)
+        if self._senders:
+            self.net.set_ghost_senders(*self.part.ghost_senders(graph))
         self.rounds = []        # global counters (summed over ranks)
         self.local_rounds = []  # this rank's engine counters (its owned peers' work)
         self.exchange_s = 0.0   # host wall time spent in the row exchange since reset
@@ -240,6 +272,8 @@ class PartitionedNetwork:
         W = (self.M + 63) // 64
         rows = max(len(self.part.send_local), len(self.part.recv_local), 1)
         self._bufs = (self.net.alloc_exchange(rows * (1 + W)), self.net.alloc_exchange(rows * (1 + W)))
+        self._fbufs = ((self.net.alloc_exchange(rows * (1 + W)), self.net.alloc_exchange(rows * (1 + W)))
+                       if self._senders else None)
         if self.world > 1 and hasattr(self.net, "set_exchange_buffer"):
             # the round packs its live rows itself: their counts arrive with the round counters,
             # so exchange_pack_live below costs no second stream drain before the sends
@@ -274,6 +308,22 @@ class PartitionedNetwork:
                 self._stream.wait_stream(torch.cuda.current_stream(t.device))
         return t
 
+    def _send_rows(self, plane):
+        p = self.part
+        # plane 0: frontier rows owner -> ghost holders; plane 1: pushes ghost -> owner
+        return p.send_counts if plane == 0 else p.recv_counts
+
+    def _senders_frontier(self):
+        """Gossip records / deliveries: the boundary peers' frontier rows of this round to the
+        ranks holding them as ghosts (plane 0), before the next round begins."""
+        R = 1 + (self.M + 63) // 64
+        send_off = np.concatenate([[0], np.cumsum(self._send_rows(0))]).astype(np.int64)
+        sbuf, rbuf = self._fbufs
+        counts = np.asarray(self.net.exchange_pack_live(0, sbuf), dtype=np.int64)
+        recv_cnt = self.transport.exchange_counts(counts)[:, self.rank].copy()
+        self.transport.exchange_records(sbuf, send_off, counts, rbuf, recv_cnt, R)
+        self.net.exchange_unpack_live(0, self._ready(rbuf), recv_cnt)
+
     def step(self):
         if not self._begun:
             self.net.step_begin()
@@ -287,12 +337,12 @@ class PartitionedNetwork:
             t0 = time.perf_counter()
             W = (self.M + 63) // 64
             R = 1 + W
-            p = self.part
             plane = self._plane
-            # plane 0: frontier rows owner -> ghost holders; plane 1: pushes ghost -> owner
-            send_rows, recv_rows = (p.send_counts, p.recv_counts) if plane == 0 else (p.recv_counts, p.send_counts)
+            send_rows = self._send_rows(plane)
             send_off = np.concatenate([[0], np.cumsum(send_rows)]).astype(np.int64)
             sbuf, rbuf = self._bufs
+            if self._senders:
+                self._senders_frontier()
             counts = np.asarray(self.net.exchange_pack_live(plane, sbuf), dtype=np.int64)
             allv = self.transport.exchange_counts(np.concatenate([counts, vals]))
             recv_cnt = allv[:, self.rank].copy()
@@ -333,6 +383,19 @@ class PartitionedNetwork:
         """(global ids, seen rows) of the peers this rank owns."""
         s = self.net.seen_plane()
         return self.part.gid[self.part.owned_local], s[self.part.owned_local]
+
+    def deliveries(self):
+        """The first receipts of the last round at the peers this rank owns, as Deliveries with
+        global peer / parent ids (sorted by (peer, msg)): this rank's share of the batched
+        node_message hook (node.py:334-338; gossip needs deliveries=True or record=True)."""
+        from .network import Deliveries
+        if self.mode == "gossip" and self.world > 1 and not self._senders:
+            raise RuntimeError("partitioned gossip deliveries need PartitionedNetwork(deliveries=True)")
+        # the local stream also holds the ghosts' receipts (their rows arrived as plane 0)
+        n = self.net.deliveries_count()
+        d = self.net.deliveries(cap=n)
+        own = (d.peer >= self.part.lo) & (d.peer < self.part.hi)
+        return Deliveries(d.peer[own], d.msg[own], d.hop[own], d.parent[own])
 
     def owned_hop_parent(self):
         hop, par = self.net.hop_parent()

@@ -233,13 +233,14 @@ def test_config3_flood_full_size_properties():
     assert sum(r.new_deliveries for r in sub) == int((hop >= 0).sum())
 
 
-def test_config4_gossip_full_size_parity():
-    """Config 4 (10M-peer Barabasi-Albert m=4, 4096 push-gossips, k=3) at full size.
-    Broadcasts are independent bit lanes, so the first 64 of the 4096 must come out exactly as
-    a 64-broadcast run: (a) the GPU 4096 run's word-0 seen bits == the GPU 64 run's delivered
-    set; (b) the GPU 64 run's hop and parent planes == the C oracle's, bit for bit; plus every
-    first receipt relays exactly 3 (min degree 4 > k) and a reset re-run is identical."""
-    from oracle import coracle
+C4_WORDS = (0, 9, 18, 27, 36, 45, 54, 63)  # spread over the 4096-broadcast row
+
+
+@pytest.fixture(scope="module")
+def c4_full():
+    """Config 4 (10M-peer Barabasi-Albert m=4, 4096 push-gossips, k=3) at full size, run once
+    per module: the graph, the origins, the whole 10M x 64-word seen plane and the per-round
+    counters of two runs (the second after a reset)."""
     from p2pnetwork.gpu import PeerGraph, make_sources
     g = PeerGraph.barabasi_albert(10_000_000, 4, seed=1)
     src = make_sources(g.V, 4096, seed=1)
@@ -247,28 +248,65 @@ def test_config4_gossip_full_size_parity():
         net.broadcast(src)
         a = net.run()
         seen = net.seen_plane()
-        words = {0: seen[:, 0].copy(), 63: seen[:, 63].copy()}
-        del seen
         net.reset()
         b = net.run()
+    return g, src, seen, a, b
+
+
+def test_config4_full_size_reset_identical(c4_full):
+    """A reset re-run is identical round for round, and every first receipt relays exactly 3
+    (min degree 4 > k: Node.send_to_node called k times, node.py:114-116)."""
+    _, _, _, a, b = c4_full
     assert [r.as_dict() for r in a] == [r.as_dict() for r in b]
     for r in a:
         assert r.relays == 3 * r.new_deliveries
-    # word 0 (messages 0..63) and word 63 (4032..4095: the Philox counters carry the global
-    # message id, so a 64-broadcast run with msg_id_base 4032 is the same experiment)
-    for w, word in words.items():
+
+
+def test_config4_full_size_counters_are_the_sum_of_its_words(c4_full):
+    """Broadcasts are independent bit lanes: each of the 64 words of the 4096-run equals a
+    64-broadcast run of its messages (global ids via msg_id_base, so the same Philox streams)
+    on one-word rows -- its seen column bit for bit -- and every additive per-round counter of
+    the 4096-run (first receipts, relays, active words, wedges, pushed masks) is the sum of the
+    64 runs' counters.  The one-word runs take the W = 1 kernels, the 4096-run the W = 64 fused
+    ones; C4_WORDS of them are pinned to the C oracle below."""
+    g, src, seen, a, _ = c4_full
+    keys = ("new_deliveries", "relays", "active_words", "wedges", "scatter_words")
+    tot = np.zeros((len(a) + 8, len(keys)), dtype=np.int64)
+    for w in range(64):
         base = 64 * w
-        with gpu_net(g, "gossip", 3, 0x5EED, record=True, msg_id_base=base) as net:
+        with gpu_net(g, "gossip", 3, 0x5EED, record=False, msg_id_base=base) as net:
             net.broadcast(src[base:base + 64])
             sub = net.run()
-            hop, parent = net.hop_parent()
-        bits = np.unpackbits(word.view(np.uint8).reshape(g.V, 8), axis=1, bitorder="little").astype(bool)
-        np.testing.assert_array_equal(bits, hop >= 0)
-        ora = coracle.run(g.rowptr, g.colidx, src[base:base + 64], "gossip", 3, 0x5EED,
-                          msg_id_base=base, record=True)
-        np.testing.assert_array_equal(hop, ora.hop)
-        np.testing.assert_array_equal(parent, ora.parent)
-        assert_rounds_equal(sub, ora.rounds)
+            col = net.seen_word(0)
+        np.testing.assert_array_equal(col, seen[:, w], err_msg=f"word {w}")
+        for i, r in enumerate(sub):
+            tot[i] += [getattr(r, k) for k in keys]
+    for j, k in enumerate(keys):
+        np.testing.assert_array_equal(trim_zeros(tot[:, j]), trim_zeros([getattr(r, k) for r in a]),
+                                      err_msg=k)
+
+
+@pytest.mark.parametrize("w", C4_WORDS)
+def test_config4_full_size_word_matches_c_oracle(c4_full, w):
+    """Word w of config 4's 4096-broadcast run (messages 64w .. 64w+63) == a 64-broadcast run
+    whose hop and parent planes (10M x 64) and per-round counters == the C oracle's, bit for bit
+    (the Philox counters carry the global message id, so msg_id_base = 64w is the same
+    experiment)."""
+    from oracle import coracle
+    g, src, seen, _, _ = c4_full
+    base = 64 * w
+    with gpu_net(g, "gossip", 3, 0x5EED, record=True, msg_id_base=base) as net:
+        net.broadcast(src[base:base + 64])
+        sub = net.run()
+        hop, parent = net.hop_parent()
+    bits = np.unpackbits(seen[:, w].copy().view(np.uint8).reshape(g.V, 8), axis=1,
+                         bitorder="little").astype(bool)
+    np.testing.assert_array_equal(bits, hop >= 0)
+    ora = coracle.run(g.rowptr, g.colidx, src[base:base + 64], "gossip", 3, 0x5EED,
+                      msg_id_base=base, record=True)
+    np.testing.assert_array_equal(hop, ora.hop)
+    np.testing.assert_array_equal(parent, ora.parent)
+    assert_rounds_equal(sub, ora.rounds)
 
 
 @pytest.mark.parametrize("push", ["atomic", "store", "auto"])

@@ -115,7 +115,7 @@ def test_partitioned_engines_match_single_gpu(kind, mode, M, thr, world, overlap
     g = graph(kind)
     src = make_sources(g.V, M, seed=21)
     kw = dict(mode=mode, fanout=3, gossip_seed=99, churn_threshold_value=thr, churn_seed=17)
-    res = run_partitioned(g, world, src, overlap=overlap, record=(mode == "flood"), **kw)
+    res = run_partitioned(g, world, src, overlap=overlap, record=True, **kw)
     with GraphNetwork(g, record=True, **kw) as one:
         one.broadcast(src)
         rounds1 = one.run()
@@ -129,16 +129,75 @@ def test_partitioned_engines_match_single_gpu(kind, mode, M, thr, world, overlap
         for k in keys:
             np.testing.assert_array_equal(trim_zeros([getattr(r, k) for r in rounds]),
                                           trim_zeros([getattr(r, k) for r in rounds1]), err_msg=k)
-    if mode == "flood":
-        hop = np.full((g.V, M), -1, np.int32)
-        par = np.full((g.V, M), -1, np.int32)
-        for _, _, _, (gids, h, p) in res:
-            hop[gids], par[gids] = h, p
-        np.testing.assert_array_equal(hop, hop1)
-        np.testing.assert_array_equal(par, par1)
+    # hop / parent of every owned peer (gossip: ghost senders' picks replayed from their global
+    # degree and adjacency order, their frontier rows exchanged as plane 0)
+    hop = np.full((g.V, M), -1, np.int32)
+    par = np.full((g.V, M), -1, np.int32)
+    for _, _, _, (gids, h, p) in res:
+        hop[gids], par[gids] = h, p
+    np.testing.assert_array_equal(hop, hop1)
+    np.testing.assert_array_equal(par, par1)
     # and the single engine against the oracle (C restatement)
     ora = coracle.run(g.rowptr, g.colidx, src, mode, 3, 99, 0, thr, 17, record=True)
     np.testing.assert_array_equal(hop1, ora.hop)
+    np.testing.assert_array_equal(par1, ora.parent)
+
+
+@pytest.mark.parametrize("kind,mode,world", [("ba", "gossip", 3), ("ws", "flood", 4), ("sparse", "gossip", 2)])
+def test_partitioned_delivery_stream(kind, mode, world):
+    """The batched node_message hook on a vertex partition: per round, the union over ranks of
+    each rank's owned first receipts (global peer ids, parent = the sender of node.py:334-338)
+    == the single engine's delivery stream, record for record."""
+    from p2pnetwork.gpu import GraphNetwork, PartitionedNetwork, make_sources
+    g = graph(kind)
+    src = make_sources(g.V, 70, seed=4)
+    kw = dict(mode=mode, fanout=3, gossip_seed=5, churn_threshold_value=200_000_000, churn_seed=9)
+    shared = {"slots": [None] * world, "barrier": threading.Barrier(world)}
+    per_rank, errors = [None] * world, []
+
+    def rank_main(rank):
+        try:
+            net = PartitionedNetwork(g, world, rank, ThreadTransport(shared, rank), deliveries=True, **kw)
+            out = []
+            with net.net:
+                net.broadcast(src)
+                while True:
+                    st = net.step()
+                    out.append(net.deliveries())
+                    if not st.new_deliveries:
+                        break
+            per_rank[rank] = out
+        except BaseException as exc:
+            errors.append(exc)
+            shared["barrier"].abort()
+
+    th = [threading.Thread(target=rank_main, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=600)
+    if errors:
+        raise errors[0]
+    with GraphNetwork(g, **kw) as one:
+        one.broadcast(src)
+        want = []
+        while True:
+            st = one.step()
+            want.append(one.deliveries())
+            if not st.active:
+                break
+    n = max(len(want), *(len(x) for x in per_rank))
+    for r in range(n):
+        got = [x[r] for x in per_rank if r < len(x)]
+        peer = np.concatenate([d.peer for d in got])
+        order = np.lexsort((np.concatenate([d.msg for d in got]), peer))
+        w = want[r] if r < len(want) else None
+        if w is None:
+            assert len(peer) == 0
+            continue
+        for f in ("peer", "msg", "hop", "parent"):
+            np.testing.assert_array_equal(np.concatenate([getattr(d, f) for d in got])[order],
+                                          getattr(w, f), err_msg=f"round {r} {f}")
 
 
 def test_partitioned_gossip_small_matches_numpy_oracle():

@@ -136,3 +136,24 @@ def test_partition_refuses_more_ranks_than_the_exchange_holds():
     g = make_graph("ws")
     with pytest.raises(ValueError, match="1..16"):
         PartitionedNetwork(g, 17, 0, transport=None, engine_factory=MockEngine)
+
+
+@pytest.mark.parametrize("world", [2, 3, 5])
+def test_ghost_senders_positions(world):
+    """VertexPartition.ghost_senders: for every local slot whose neighbour u is a ghost, the
+    row owner's position in u's GLOBAL ascending adjacency and u's global degree (what replaying
+    a remote gossip sender's Floyd picks needs, node.py:114-120); -1 for local neighbours."""
+    from p2pnetwork.gpu import PeerGraph
+    from p2pnetwork.gpu.partition import VertexPartition
+    g = PeerGraph.barabasi_albert(2000, 3, seed=world)
+    for r in range(world):
+        P = VertexPartition(g, world, r)
+        gdeg, pos = P.ghost_senders(g)
+        nb = P.gid[P.colidx].astype(np.int64)
+        owner = P.gid[np.searchsorted(P.rowptr, np.arange(len(P.colidx)), side="right") - 1]
+        remote = (nb < P.lo) | (nb >= P.hi)
+        assert np.array_equal(pos >= 0, remote)
+        for j in np.nonzero(remote)[0]:
+            row = g.colidx[g.rowptr[nb[j]]:g.rowptr[nb[j] + 1]]
+            assert row[pos[j]] == owner[j]
+            assert gdeg[P.colidx[j]] == len(row)
