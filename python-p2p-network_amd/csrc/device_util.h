@@ -296,6 +296,13 @@ int grid_tasks(int64_t ntasks) {
 // receipts per peer): P2PG_FUSED_GRID (default 32) x the blocks resident at once, so that
 // blocks finishing early are replaced (measured on config 4: 2x -> 300 ms, 8x -> 267 ms,
 // 32x -> 260 ms for the fused rounds).
+// The fused / grouped kernels keep their per-wave round totals in 32 bits.  A 32-peer task adds
+// at most 32 peers x 4096 messages x fanout 16 = 2^21 to any of them (relays; hubs, deg > HUB_T,
+// never go through these kernels, so wedges <= 32 x 64 words x 512 = 2^20), so no wave may take
+// more than 2^11 tasks: the grid is never smaller than that bound asks, whatever P2PG_FUSED_GRID,
+// the device size or V (config 4: ~2.4 tasks per wave).
+constexpr int64_t TASKS_PER_WAVE_MAX = 2048;
+
 template <class F>
 int balanced_grid(F kernel, int64_t ntasks) {
   static const int gmul = [] {
@@ -303,8 +310,9 @@ int balanced_grid(F kernel, int64_t ntasks) {
     const int v = e ? std::atoi(e) : 32;
     return v > 0 ? v : 32;
   }();
-  return (int)std::min<int64_t>((int64_t)grid_tasks_uncapped(ntasks),
-                                (int64_t)gmul * resident_blocks(kernel));
+  const int64_t full = (int64_t)grid_tasks_uncapped(ntasks);
+  const int64_t floor32 = (ntasks + TASKS_PER_WAVE_MAX * WPB - 1) / (TASKS_PER_WAVE_MAX * WPB);
+  return (int)std::min<int64_t>(full, std::max<int64_t>((int64_t)gmul * resident_blocks(kernel), floor32));
 }
 
 

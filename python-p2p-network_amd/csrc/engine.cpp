@@ -33,6 +33,9 @@ struct p2pg_engine {
   p2pg_config cfg{};
   std::string err;
   int64_t V = 0, nnz = 0;
+  int64_t v_conn = 0;          // peers with >= 1 connection: the ones a round can make active
+                               // (the dense-round test compares active peers with these, so
+                               // isolated peers do not keep a run sparse)
   int32_t M = 0, W = 0;
   std::vector<int64_t> h_rowptr;
   std::vector<int32_t> h_colidx;  // host copy of the adjacency (topology updates, snapshots)
@@ -73,7 +76,9 @@ struct p2pg_engine {
   // synchronisation per round); pack_live then only hands them over
   void* auto_buf = nullptr;
   int32_t auto_plane = -1;
-  int32_t auto_round = -1;           // the round whose records auto_buf / h_seg_cnt hold
+  int32_t auto_round = -1;           // the round whose records auto_buf / auto_cnt hold
+  int64_t auto_cnt[P2PG_MAX_RANKS] = {0};  // their counts per destination (h_seg_cnt is reused
+                                           // by explicit packs of the other plane)
   bool begun = false;                 // p2pg_step_begin ran this round's phase 0
   bool last_push_e = false;    // gossip: pushes of the previous round went to E (dense)
   double e_thresh = 0.06;      // store-mode when active words >= thresh * active rows * W;
@@ -81,7 +86,7 @@ struct p2pg_engine {
                                // (c4 A/B, interleaved runs: 0.04 320.4 ms vs 0.1 324.3 ms, round 1;
                                // with the lane-parallel sparse push (round 2) W = 64: 0.04 / 0.06 /
                                // 0.08 -> 278.4 / 275.5 / 275.2 ms, W = 8: 89.1 / 89.4 / 89.5 ms)
-  double v_thresh = 0.3;       // ... and active rows >= v_thresh * V (by row width, alloc_state;
+  double v_thresh = 0.3;       // ... and active rows >= v_thresh * v_conn (by row width, alloc_state;
   double v_thresh_env = -1.0;  // P2PG_V_THRESH overrides): a dense round visits every
                                // unsaturated peer, a sparse one only the pushed-to rows (narrow
                                // rows: word density alone is high whenever anything is active)
@@ -386,7 +391,7 @@ bool wide_atomic_on(const p2pg_engine* e) {
 // changes the push form of one round, never a result.
 bool predict_dense(const p2pg_engine* e) {
   if (e->prev2_aw == 0 || e->prev2_av == 0 || e->last_new <= e->prev2_new) return false;
-  const double V = (double)e->V;
+  const double V = (double)e->v_conn;
   const double in1 = V - (double)e->prev_av, in2 = V - (double)e->prev2_av;
   if (in2 <= 0.0) return false;
   const double est_av = V - in1 * (in1 / in2);
@@ -601,6 +606,8 @@ int upload_graph(p2pg_engine* e, int64_t V, const int64_t* rowptr, const int32_t
   free_topology(e);
   e->V = V;
   e->nnz = nnz;
+  e->v_conn = 0;
+  for (int64_t v = 0; v < V; ++v) e->v_conn += rowptr[v + 1] > rowptr[v];
   if (!rev.empty()) {
     HIPCHK(e, hipMalloc((void**)&e->d_rev, sizeof(uint32_t) * rev.size()));
     HIPCHK(e, hipMemcpy(e->d_rev, rev.data(), sizeof(uint32_t) * rev.size(), hipMemcpyHostToDevice));
@@ -656,6 +663,10 @@ int upload_graph(p2pg_engine* e, int64_t V, const int64_t* rowptr, const int32_t
     }
     e->hp = HubPlan{e->d_hub_items, (int64_t)items.size(), e->d_hubs, e->d_hub_begin,
                     (int64_t)hubs.size(), e->d_partial};
+    // the fused kernels' push modes skip the H peers and push them through wide_big
+    // (launch_wide_push_e): the two sets must be the same peers
+    if (hubs.size() != wide_big.size() || !std::equal(hubs.begin(), hubs.end(), wide_big.begin()))
+      return fail(e, P2PG_ERR_STATE, "load_csr: pull hubs and wide push sources differ");
   }
   HIPCHK(e, hipMalloc((void**)&e->d_hub, sizeof(int64_t) * (hub.empty() ? 1 : hub.size())));
   if (!hub.empty())
@@ -840,7 +851,7 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
     const bool dense_pred = e->push_mode == 2 ||
         (e->push_mode == 0 && e->prev_av > 0 &&
          (double)e->prev_aw >= e->e_thresh * (double)e->prev_av * (double)e->W &&
-         (double)e->prev_av >= e->v_thresh * (double)e->V);
+         (double)e->prev_av >= e->v_thresh * (double)e->v_conn);
     fused_round = !e->d_gid && dense_pred && gossip_fused_supported(s);
     if (fused_round) {
       // a frontier nobody observes is not stored: inside p2pg_run (not its last allowed
@@ -909,7 +920,7 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
         have_tot = true;
         use_e = (double)tot[ST_ACTIVE_W] >=
                 e->e_thresh * (double)tot[ST_ACTIVE_V] * (double)e->W && tot[ST_ACTIVE_V] > 0 &&
-                (double)tot[ST_ACTIVE_V] >= e->v_thresh * (double)e->V;
+                (double)tot[ST_ACTIVE_V] >= e->v_thresh * (double)e->v_conn;
       }
     }
     // the lane-parallel sparse push sizes its (peer, word) list by the frontier's word count
@@ -945,6 +956,8 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
   }
   if ((rc = read_stats())) return rc;
   if ((rc = check_scatter_list(e, e->h_stats[STAT_COUNT]))) return rc;
+  if (e->auto_round == e->round)  // the round's own pack landed with its counters
+    for (int q = 0; q + 1 < (int)e->send_seg.size(); ++q) e->auto_cnt[q] = (int64_t)e->h_seg_cnt[q];
 #ifdef P2PG_PROF
   if (fused_round && s.prof && std::getenv("P2PG_PROF_ROUNDS")) {
     // development builds: per-round fused-kernel segment clocks (then reset)
@@ -1238,7 +1251,7 @@ int p2pg_exchange_pack_live(p2pg_engine* e, int32_t plane, void* dev_buf, int64_
   const int nseg = (int)e->send_seg.size() - 1;
   if (dev_buf == e->auto_buf && plane == e->auto_plane && e->auto_round == e->round - 1) {
     // packed by the round itself (p2pg_set_exchange_buffer), counts read with its counters
-    for (int q = 0; q < nseg; ++q) counts[q] = (int64_t)e->h_seg_cnt[q];
+    for (int q = 0; q < nseg; ++q) counts[q] = e->auto_cnt[q];
     e->auto_round = -1;  // handed over once
     return P2PG_OK;
   }

@@ -1519,9 +1519,9 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
   const uint64_t fm = valid ? full_mask(lane, W, st.M) : 0ull;
   // per-lane counters are 32-bit and per task (<= 32 peers, none a hub: no overflow), folded
   // into wave-uniform 64-bit totals after each task (fewer live VGPRs than 64-bit lanes)
-  // wave totals in 32 bits (8 fewer scalar registers): a wave of a balanced grid (<= 32 x the
-  // resident blocks) covers few tasks -- c4: ~2.4 -- so even 10^9 peers keep its relay / wedge
-  // sums (<= tasks x 32 peers x 4096 messages x fanout 16; hubs excluded) far below 2^32
+  // wave totals in 32 bits (8 fewer scalar registers): balanced_grid never gives a wave more
+  // than TASKS_PER_WAVE_MAX tasks, which keeps its relay / wedge sums (<= tasks x 32 peers x 4096
+  // messages x fanout 16; hubs excluded) below 2^32 (c4: ~2.4 tasks per wave)
   uint32_t tot[STAT_N] = {0, 0, 0, 0, 0, 0, 0, 0};
   PROF_DECL
 
@@ -2139,6 +2139,9 @@ __global__ __launch_bounds__(256) void k_unpack_live(DevState st, int plane, int
     int p = 0;
     for (int q = 1; q < nseg; ++q) p += i >= ro.off[q];
     const int64_t idx = ldc(in + i * R);
+    // a record must name a row of its source's list segment (the host checked the counts; a
+    // corrupt index is dropped here rather than written out of bounds)
+    if (idx < 0 || idx >= ldc(list_off + p + 1) - ldc(list_off + p)) continue;
     const int64_t v = ids[ldc(list_off + p) + idx];
     for (int w = lane; w < W; w += 64) {
       const uint64_t x = (uint64_t)in[i * R + 1 + w];
@@ -2360,6 +2363,15 @@ void scatter_dispatch(int grid, const DevGraph& g, const DevState& st, const Rou
 
 static bool grouped_enabled();
 
+// The push modes of the fused / grouped kernels (push-only, update+push) skip the pull hubs
+// (g.H: deg > HUB_T) and leave their pushes to launch_wide_push_e over wide_big (the same deg >
+// HUB_T set, checked equal when the graph is uploaded).  Both launchers take that path only when
+// the hub pushes can actually run: their chunk items and ids are there, and so is the H bitmap.
+static bool hub_pushes_ready(const DevGraph& g, const int64_t* big_items, int64_t n_big,
+                             const int32_t* wide_big, int64_t n_wide_big) {
+  return (n_big == 0 || (big_items && wide_big)) && (n_wide_big == 0 || g.H != nullptr);
+}
+
 hipError_t launch_gossip_scatter(const DevGraph& g, const DevState& st, const RoundParams& p,
                                  const int64_t* hub_items, int64_t n_hub_items, bool store_e,
                                  hipStream_t s, const int64_t* big_items, int64_t n_big,
@@ -2376,8 +2388,8 @@ hipError_t launch_gossip_scatter(const DevGraph& g, const DevState& st, const Ro
     const char* e = std::getenv("P2PG_PUSH_GROUPED");
     return !(e && std::strcmp(e, "0") == 0);
   }();
-  if (store_e && push_grouped && grouped_enabled() && st.W <= GROUPED_W_MAX &&
-      (n_big == 0 || (big_items && wide_big))) {
+  const bool hubs_ok = hub_pushes_ready(g, big_items, n_big, wide_big, n_wide_big);
+  if (store_e && push_grouped && grouped_enabled() && st.W <= GROUPED_W_MAX && hubs_ok) {
     hipError_t r = launch_gossip_push_grouped(g, st, p, s);
     if (r != hipSuccess) return r;
     return launch_wide_push_e(g, st, p, big_items, n_big, wide_big, n_wide_big, s);
@@ -2387,8 +2399,7 @@ hipError_t launch_gossip_scatter(const DevGraph& g, const DevState& st, const Ro
     const char* e = std::getenv("P2PG_PUSH_FUSED");
     return !(e && std::strcmp(e, "0") == 0);
   }();
-  if (store_e && push_fused && st.W <= 64 && st.AW[p.round & 1] != nullptr &&
-      (n_big == 0 || (big_items && wide_big))) {
+  if (store_e && push_fused && st.W <= 64 && st.AW[p.round & 1] != nullptr && hubs_ok) {
 #define P2PG_FUSED_PO(CH, KK)                                                                       \
   hipLaunchKernelGGL((k_gossip_fused<CH, KK, 1>),                                                 \
                      dim3(balanced_grid(k_gossip_fused<CH, KK, 1>, (g.V + 31) >> 5)), dim3(256),    \
@@ -2432,8 +2443,8 @@ bool gossip_update_push_supported(const DevState& st) {
 hipError_t launch_gossip_update_push(const DevGraph& g, const DevState& st, const RoundParams& p,
                                      const int64_t* big_items, int64_t n_big,
                                      const int32_t* wide_big, int64_t n_wide_big, hipStream_t s) {
-  if (!gossip_update_push_supported(st) || p.phase >= 0 || (n_big && !(big_items && wide_big)) ||
-      (n_wide_big && !g.H))
+  if (!gossip_update_push_supported(st) || p.phase >= 0 ||
+      !hub_pushes_ready(g, big_items, n_big, wide_big, n_wide_big))
     return hipErrorInvalidValue;
 #define P2PG_FUSED_UP(CH, KK)                                                                       \
   hipLaunchKernelGGL((k_gossip_fused<CH, KK, 2>),                                                 \

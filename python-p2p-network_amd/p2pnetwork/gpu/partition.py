@@ -230,6 +230,8 @@ class PartitionedNetwork:
         # sender), and for a ghost sender the rank needs its frontier rows (plane 0 travels
         # too, owner -> ghost holders) and its global degree / adjacency order
         self._senders = mode == "gossip" and world > 1 and (record or deliveries)
+        self._deliv = deliveries
+        self._last_deliv = None
         self.deg = graph.degree().astype(np.int32)  # global degrees (round-0 counters); the
         # global graph itself is not kept: the engine holds only the rank-local CSR
         self.mode, self.fanout = mode, fanout
@@ -330,6 +332,10 @@ class PartitionedNetwork:
         st = self.net.step_end()
         self._begun = False
         self.local_rounds.append(st)
+        if self._deliv:
+            # before the next round begins (its interior peers overwrite the frontier plane the
+            # parents of this round's receipts are read from)
+            self._last_deliv = self._owned_deliveries()
         vals = np.asarray([getattr(st, f) for f in STAT_FIELDS[2:]], dtype=np.int64)
         if self.world == 1:
             tot = vals
@@ -387,10 +393,14 @@ class PartitionedNetwork:
     def deliveries(self):
         """The first receipts of the last round at the peers this rank owns, as Deliveries with
         global peer / parent ids (sorted by (peer, msg)): this rank's share of the batched
-        node_message hook (node.py:334-338; gossip needs deliveries=True or record=True)."""
+        node_message hook (node.py:334-338).  Needs PartitionedNetwork(deliveries=True): they are
+        taken inside step(), before the next round's interior peers start."""
+        if not self._deliv:
+            raise RuntimeError("partitioned deliveries need PartitionedNetwork(deliveries=True)")
+        return self._last_deliv
+
+    def _owned_deliveries(self):
         from .network import Deliveries
-        if self.mode == "gossip" and self.world > 1 and not self._senders:
-            raise RuntimeError("partitioned gossip deliveries need PartitionedNetwork(deliveries=True)")
         # the local stream also holds the ghosts' receipts (their rows arrived as plane 0)
         n = self.net.deliveries_count()
         d = self.net.deliveries(cap=n)
