@@ -104,6 +104,9 @@ struct p2pg_engine {
   uint64_t prev_aw = 0, prev_av = 0;  // active words / rows of the previous round
   uint64_t last_new = 0;       // first receipts of the last round run
   uint64_t prev2_aw = 0, prev2_av = 0, prev2_new = 0;  // the same, one round earlier
+  uint64_t prev_sw = 0;        // distinct masks pushed in the last round (>= the next frontier's
+                               // nonzero words: each of them received at least one)
+  bool saw_dense = false;      // a round of this run pushed into E (the dense phase has begun)
   int update_push = -1;        // the first dense round after a sparse one: its update and its
                                // E pushes in one pass (launch_gossip_update_push) -- -1 when the
                                // round is predicted dense (predict_dense), 0 never, 1 whenever
@@ -140,6 +143,11 @@ struct p2pg_engine {
   uint32_t* d_chunk_cnt = nullptr;  // per list chunk: pairs, and their offsets
   uint64_t* d_chunk_off = nullptr;
   bool wlist_check = false;     // a sparse scatter ran this round: check its count after it
+  // p2pg_run's decay-phase batches: round counters of up to BATCH_MAX rounds (one slot each)
+  unsigned long long* d_bstats = nullptr;
+  unsigned long long* h_bstats = nullptr;  // pinned
+  int batch_rounds = -1;        // P2PG_RUN_BATCH (rounds per host synchronisation in the decay
+                                // phase; 1 = none), -1 = the default
 };
 
 namespace {
@@ -400,6 +408,34 @@ bool predict_dense(const p2pg_engine* e) {
          est_av >= e->v_thresh * V;
 }
 
+// Will this round's pushes go by row atomics whatever its counters say?  Then the push is
+// launched without reading them first (one host synchronisation per round instead of two): in
+// the decay phase (after the dense rounds, receipts shrinking) and while the rising frontier is
+// far below the dense-round thresholds (active peers, grown twice by the last growth factor, under
+// half of v_thresh * v_conn).  Only the push form depends on it, never a result.
+bool clearly_sparse(const p2pg_engine* e) {
+  if (e->round == 0) return false;  // (origination: the counters are the host's)
+  if (e->saw_dense) return e->last_new < e->prev2_new;
+  if (e->prev_av == 0) return true;  // nothing arrives: an empty round
+  const double grow = e->prev2_av ? std::max(1.0, (double)e->prev_av / (double)e->prev2_av) : 64.0;
+  return (double)e->prev_av * grow * grow < 0.5 * e->v_thresh * (double)e->v_conn;
+}
+
+// A dense round follows a dense round if the frontier it will push is still dense by the rule
+// the engine applies to its own counters (use_e in p2pg_step).  The counters are those of the
+// round before; in the decay phase (receipts shrinking) they are first shrunk by their last
+// factor, so the last dense round is not one round late (c4: round 24's 3.0e7 active words are
+// below 0.06 x 8.2e6 peers x 64, while round 23's were above).  Only the push form depends on
+// it, never a result.
+bool still_dense(const p2pg_engine* e) {
+  double aw = (double)e->prev_aw, av = (double)e->prev_av;
+  if (e->saw_dense && e->last_new < e->prev2_new && e->prev2_aw && e->prev2_av) {
+    aw *= aw / (double)e->prev2_aw;
+    av *= av / (double)e->prev2_av;
+  }
+  return av > 0.0 && aw >= e->e_thresh * av * (double)e->W && av >= e->v_thresh * (double)e->v_conn;
+}
+
 // Run this round's update and its (dense) pushes in one pass?
 bool update_push_round(const p2pg_engine* e, const RoundParams& p) {
   if (e->update_push == 0 || e->cfg.mode != P2PG_MODE_GOSSIP || e->push_mode != 0 || e->d_gid ||
@@ -528,6 +564,7 @@ int p2pg_create(const p2pg_config* cfg, p2pg_engine** out) {
   if (const char* f = std::getenv("P2PG_PUSH_DEDUP")) e->push_dedup = std::atoi(f);
   if (const char* f = std::getenv("P2PG_WIDE_ATOMIC")) e->wide_atomic = std::strcmp(f, "0") != 0;
   if (const char* f = std::getenv("P2PG_UPDATE_PUSH")) e->update_push = std::atoi(f);
+  if (const char* f = std::getenv("P2PG_RUN_BATCH")) e->batch_rounds = std::atoi(f);
   if (const char* m = std::getenv("P2PG_GOSSIP_PUSH"))
     e->push_mode = !std::strcmp(m, "atomic") ? 1 : (!std::strcmp(m, "store") ? 2 : 0);
   HIPCHK(e, hipSetDevice(cfg->device));
@@ -746,6 +783,8 @@ int p2pg_reset(p2pg_engine* e) {
   e->prev_aw = e->prev_av = 0;
   e->last_new = 0;
   e->prev2_aw = e->prev2_av = e->prev2_new = 0;
+  e->prev_sw = 0;
+  e->saw_dense = false;
   for (int i = 0; i < P2PG_KCLASS_N; ++i) {
     e->kms[i] = 0;
     e->klaunch[i] = 0;
@@ -848,10 +887,7 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
     // previous round stored per-edge masks: gather them (pull, no atomics).  If this round is
     // predicted dense as well (the previous round's word density; the prediction only picks
     // the push form, never the result), the same pass also pushes this round's receipts.
-    const bool dense_pred = e->push_mode == 2 ||
-        (e->push_mode == 0 && e->prev_av > 0 &&
-         (double)e->prev_aw >= e->e_thresh * (double)e->prev_av * (double)e->W &&
-         (double)e->prev_av >= e->v_thresh * (double)e->v_conn);
+    const bool dense_pred = e->push_mode == 2 || (e->push_mode == 0 && still_dense(e));
     fused_round = !e->d_gid && dense_pred && gossip_fused_supported(s);
     if (fused_round) {
       // a frontier nobody observes is not stored: inside p2pg_run (not its last allowed
@@ -912,10 +948,14 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
     // push form for this round's sends: row atomics when the frontier is sparse, whole-row
     // edge-mask stores (+ pull next round) when most words of the active rows are set
     bool use_e = false, have_tot = false;
+    // the counters of this round are needed before its push only to choose the form (unless
+    // that choice is clear already) and to size the sparse push's (peer, word) list (else
+    // bounded by the last round's pushed masks)
+    const bool blind = e->round > 0 && e->push_mode != 2 && clearly_sparse(e) && e->prev_sw > 0;
     if (s.E[0] && !e->d_gid) {  // partitioned gossip pushes by row atomics (ghost rows travel)
       if (e->push_mode == 2) {
         use_e = true;
-      } else if (e->push_mode == 0) {
+      } else if (e->push_mode == 0 && !blind) {
         if ((rc = read_stats())) return rc;
         have_tot = true;
         use_e = (double)tot[ST_ACTIVE_W] >=
@@ -924,16 +964,23 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
       }
     }
     // the lane-parallel sparse push sizes its (peer, word) list by the frontier's word count
-    if (!use_e && !have_tot && sparse_scatter_on(e) && (rc = read_stats())) return rc;
+    if (!use_e && !have_tot && !blind && sparse_scatter_on(e)) {
+      if ((rc = read_stats())) return rc;
+      have_tot = true;
+    }
     // decay phase (fewer first receipts than the round before): most pushes are duplicates,
-    // so the sparse push drops seen bits before its atomics (RoundParams::dedup_push)
+    // so the sparse push drops seen bits before its atomics (RoundParams::dedup_push; without
+    // this round's counters: the phase of the rounds before)
     if (!use_e && sparse_scatter_on(e))
-      p.dedup_push = e->push_dedup == 1 || (e->push_dedup < 0 && tot[ST_NEW] < e->last_new);
+      p.dedup_push = e->push_dedup == 1 ||
+                     (e->push_dedup < 0 && (have_tot ? tot[ST_NEW] < e->last_new
+                                                     : e->saw_dense && e->last_new < e->prev2_new));
+    const uint64_t list_words = have_tot ? tot[ST_ACTIVE_W] : e->prev_sw;
     if ((rc = timed(e, use_e ? 6 : 2, [&] {
            return use_e ? launch_gossip_scatter(g, s, p, e->d_hub, e->n_hub, true, e->stream,
                                                 e->d_hub_big, e->n_hub_big, e->d_wide_big,
                                                 e->n_wide_big)
-                        : launch_scatter_atomic(e, g, p, tot[ST_ACTIVE_W]);
+                        : launch_scatter_atomic(e, g, p, list_words);
          })))
       return rc;
     e->last_push_e = use_e;
@@ -995,12 +1042,114 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
   e->prev_aw = tot[ST_ACTIVE_W];
   e->prev_av = tot[ST_ACTIVE_V];
   e->last_new = tot[ST_NEW];
+  e->prev_sw = tot[ST_SCATTER];
+  if (e->last_push_e) e->saw_dense = true;
   e->round += 1;
   if (!active && !(e->cfg.flags & P2PG_FLAG_NO_AUTOSTOP)) e->done = true;
   return active ? 1 : 0;
 }
 
 int p2pg_step_end(p2pg_engine* e, p2pg_round_stats* out) { return p2pg_step(e, out); }
+
+// p2pg_run's decay phase: after the dense rounds, while receipts shrink, every round is an update
+// of the row pushes and a row-atomic push whose form, list bound (the last round's pushed masks,
+// shrinking too) and dedup setting need none of its own counters -- so BATCH_MAX of them are
+// enqueued at once, each writing its counters to its own slot, and read with ONE host
+// synchronisation (c4: ~20 tail rounds of 0.05-0.2 ms kernels each paid a full host round trip).
+// Rounds enqueued after the run went quiet see an empty frontier and change nothing; they are
+// not reported and the engine stands where p2pg_step would have left it.  A (peer, word) list
+// that could not hold a round's frontier fails the call loudly (P2PG_ERR_STATE).
+constexpr int BATCH_MAX = 8;
+
+static bool decay_batchable(const p2pg_engine* e) {
+  const int br = e->batch_rounds < 0 ? BATCH_MAX : e->batch_rounds;
+  return br > 1 && e->have_state && !e->done && !e->begun && e->round > 0 &&
+         e->cfg.mode == P2PG_MODE_GOSSIP && e->saw_dense && !e->last_push_e &&
+         e->last_new < e->prev2_new && e->prev_sw > 0 && !e->consume_next && e->arr_round < 0 &&
+         !e->d_gid && !(e->cfg.flags & P2PG_FLAG_NO_AUTOSTOP) && e->push_mode != 2 &&
+         e->auto_buf == nullptr && sparse_scatter_on(e) &&
+         e->last_new * 16 < (uint64_t)e->V;  // the tail: small rounds, where the syncs dominate
+}
+
+static int run_decay_batch(p2pg_engine* e, int32_t R, p2pg_round_stats* out, int32_t* ran) {
+  constexpr size_t SLOT = STAT_COUNT + 1;  // counters + the sparse list's fill count
+  DevState& s = e->st;
+  HIPCHK(e, hipSetDevice(e->cfg.device));
+  if (!e->d_bstats) {
+    HIPCHK(e, hipMalloc((void**)&e->d_bstats, sizeof(unsigned long long) * SLOT * BATCH_MAX));
+    HIPCHK(e, hipHostMalloc((void**)&e->h_bstats, sizeof(unsigned long long) * SLOT * BATCH_MAX));
+  }
+  HIPCHK(e, hipMemsetAsync(e->d_bstats, 0, sizeof(unsigned long long) * SLOT * R, e->stream));
+  // the list, sized once for the batch by the first round's bound
+  SparseBufs b;
+  hipError_t lr = sparse_bufs(e, (int64_t)e->prev_sw, b);
+  if (lr != hipSuccess) return fail(e, P2PG_ERR_HIP, std::string("run (batch list): ") + hipGetErrorString(lr));
+  const uint64_t words = (uint64_t)e->wlist_cap;  // no round of the batch grows the list
+  unsigned long long* const stats0 = s.stats;
+  const DevGraph g = graph(e);
+  int rc = P2PG_OK;
+  for (int32_t i = 0; i < R && rc == P2PG_OK; ++i) {
+    s.stats = e->d_bstats + SLOT * i;
+    RoundParams p = params(e);
+    p.round = e->round + i;
+    rc = timed(e, 4, [&] { return launch_gossip_update(g, s, p, e->stream); });
+    if (rc == P2PG_OK && s.hop) rc = timed(e, 3, [&] { return launch_record(g, s, p, e->stream); });
+    p.dedup_push = e->push_dedup != 0;  // decay phase
+    if (rc == P2PG_OK)
+      rc = timed(e, 2, [&] {
+        return launch_scatter_atomic(e, g, p, std::min<uint64_t>(e->prev_sw, words));
+      });
+  }
+  s.stats = stats0;
+  e->wlist_check = false;
+  if (rc) return rc;
+  HIPCHK(e, hipMemcpyAsync(e->h_bstats, e->d_bstats, sizeof(unsigned long long) * SLOT * R,
+                           hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  if ((rc = resolve_timings(e))) return rc;
+  *ran = 0;
+  for (int32_t i = 0; i < R; ++i) {
+    const unsigned long long* h = e->h_bstats + SLOT * i;
+    if ((int64_t)h[STAT_COUNT] > e->wlist_cap)
+      return fail(e, P2PG_ERR_STATE, "run: a batched round's frontier outgrew the sparse push list (" +
+                                         std::to_string(h[STAT_COUNT]) + " words listed, room for " +
+                                         std::to_string(e->wlist_cap) + ")");
+    uint64_t tot[STAT_N] = {0};
+    for (int sh = 0; sh < STAT_SHARDS; ++sh)
+      for (int q = 0; q < STAT_N; ++q) tot[q] += h[sh * STAT_N + q];
+    const bool active = tot[ST_NEW] != 0;
+    p2pg_round_stats& o = out[i];
+    o.round = e->round;
+    o.active = active ? 1 : 0;
+    o.new_deliveries = tot[ST_NEW];
+    o.relays = tot[ST_RELAYS];
+    o.active_vertices = tot[ST_ACTIVE_V];
+    o.active_words = tot[ST_ACTIVE_W];
+    o.wedges = tot[ST_WEDGES];
+    o.deg_active = tot[ST_DEG_ACT];
+    o.scatter_words = tot[ST_SCATTER];
+    o.touched_words = tot[ST_AUX];
+    o.push_form = P2PG_PUSH_ATOMIC;
+    o.reserved_ = 0;
+    e->total_relays += tot[ST_RELAYS];
+    e->frontier_kept_prev = e->frontier_kept;
+    e->frontier_kept = true;
+    e->prev2_aw = e->prev_aw;
+    e->prev2_av = e->prev_av;
+    e->prev2_new = e->last_new;
+    e->prev_aw = tot[ST_ACTIVE_W];
+    e->prev_av = tot[ST_ACTIVE_V];
+    e->last_new = tot[ST_NEW];
+    e->prev_sw = tot[ST_SCATTER];
+    e->round += 1;
+    *ran = i + 1;
+    if (!active) {
+      e->done = true;  // (rounds enqueued after this one saw an empty frontier)
+      break;
+    }
+  }
+  return P2PG_OK;
+}
 
 int p2pg_run(p2pg_engine* e, int32_t max_rounds, p2pg_round_stats* per_round,
              int32_t* n_rounds) {
@@ -1009,6 +1158,18 @@ int p2pg_run(p2pg_engine* e, int32_t max_rounds, p2pg_round_stats* per_round,
   int rc = 1;
   while (n < max_rounds) {
     p2pg_round_stats tmp;
+    if (decay_batchable(e) && max_rounds - n >= 2) {
+      const int br = e->batch_rounds < 0 ? BATCH_MAX : std::min(e->batch_rounds, BATCH_MAX);
+      const int32_t R = std::min<int32_t>(br, max_rounds - n);
+      p2pg_round_stats buf[BATCH_MAX];
+      int32_t ran = 0;
+      if ((rc = run_decay_batch(e, R, buf, &ran)) < 0) return rc;
+      if (per_round) std::memcpy(per_round + n, buf, sizeof(p2pg_round_stats) * ran);
+      n += ran;
+      rc = e->done ? 0 : 1;
+      if (rc == 0) break;
+      continue;
+    }
     // only the last two rounds a call may run can leave frontiers behind for the caller (the
     // deliveries of the last round and their parents in the round before; snapshots); a
     // quiescent round has none
@@ -1688,6 +1849,8 @@ void p2pg_destroy(p2pg_engine* e) {
   free_state(e);
   free_graph(e);
   if (e->h_stats) (void)hipHostFree(e->h_stats);
+  if (e->h_bstats) (void)hipHostFree(e->h_bstats);
+  if (e->d_bstats) (void)hipFree(e->d_bstats);
   for (int i = 0; i < 2; ++i)
     if (e->ev[i]) (void)hipEventDestroy(e->ev[i]);
   for (hipEvent_t ev : e->ev_pool) (void)hipEventDestroy(ev);

@@ -1,0 +1,78 @@
+"""GPU: the host-side round schedule changes nothing.  p2pg_run enqueues several decay-phase
+rounds per host synchronisation (run_decay_batch) and p2pg_step launches a sparse round's push
+without reading its counters first when the push form is clear (clearly_sparse, bounded list);
+both only decide WHEN the host looks at the counters, so every per-round counter (the
+message_count_send sums of node.py:114-116) and every seen bit must equal a run that reads them
+each round (P2PG_RUN_BATCH=1, step by step), and the C oracle."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+FIELDS = ("new_deliveries", "relays", "active_vertices", "active_words", "wedges", "deg_active",
+          "scatter_words", "touched_words")
+
+
+def _net(g, thr, **kw):
+    from p2pnetwork.gpu import GraphNetwork
+    return GraphNetwork(g, mode="gossip", fanout=3, gossip_seed=0x5EED, churn_threshold_value=thr,
+                        churn_seed=0xC0FFEE, **kw)
+
+
+def _log(msg):
+    import sys
+    import time
+    print(f"[{time.strftime('%H:%M:%S')}] {msg}", flush=True)
+    sys.stdout.flush()
+
+
+def _rows(rounds):
+    return [tuple(getattr(r, f) for f in FIELDS) for r in rounds]
+
+
+@pytest.mark.parametrize("thr", [0, 200_000_000])
+def test_batched_and_blind_rounds_equal_round_by_round(thr, monkeypatch):
+    from oracle import coracle
+    from p2pnetwork.gpu import PeerGraph, make_sources
+    g = PeerGraph.barabasi_albert(1_000_000, 4, seed=5)
+    src = make_sources(g.V, 4096, seed=3)
+    with _net(g, thr) as net:                         # p2pg_run: batched decay tail
+        net.broadcast(src)
+        a = net.run()
+        _log(f"batched run: {len(a)} rounds")
+        seen_a = net.seen_plane()
+        assert len(net.deliveries(cap=16)) == 0       # quiescent: no receipts in the last round
+        net.reset()
+        chunked = []
+        while True:                                   # p2pg_run in chunks of 3 rounds
+            part = net.run(max_rounds=3)
+            chunked += part
+            if not part[-1].active:
+                break
+        seen_c = net.seen_plane()
+        _log(f"chunked run: {len(chunked)} rounds")
+    monkeypatch.setenv("P2PG_RUN_BATCH", "1")
+    with _net(g, thr) as net:                         # p2pg_run, one synchronisation per round
+        net.broadcast(src)
+        b = net.run()
+        _log(f"unbatched run: {len(b)} rounds")
+        seen_b = net.seen_plane()
+    with _net(g, thr) as net:                         # p2pg_step, one round per call
+        net.broadcast(src)
+        c = []
+        while True:
+            st = net.step()
+            c.append(st)
+            if not st.active:
+                break
+        seen_s = net.seen_plane()
+        _log(f"step run: {len(c)} rounds")
+    assert _rows(a) == _rows(b) == _rows(c) == _rows(chunked)
+    for s in (seen_b, seen_c, seen_s):
+        np.testing.assert_array_equal(seen_a, s)
+    _log("oracle")
+    ora = coracle.run(g.rowptr, g.colidx, src, "gossip", 3, 0x5EED, 0, thr, 0xC0FFEE, record=False,
+                      want_seen=True)
+    np.testing.assert_array_equal(seen_a, ora.seen)
+    want = [tuple(r[f] for f in FIELDS[:-1]) for r in ora.rounds]
+    assert [x[:-1] for x in _rows(a)][:len(want)] == want
