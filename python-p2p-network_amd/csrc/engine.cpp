@@ -107,6 +107,8 @@ struct p2pg_engine {
   uint64_t prev_sw = 0;        // distinct masks pushed in the last round (>= the next frontier's
                                // nonzero words: each of them received at least one)
   bool saw_dense = false;      // a round of this run pushed into E (the dense phase has begun)
+  bool decay_pred = true;      // still_dense shrinks the counters in the decay phase
+                               // (P2PG_DECAY_PRED=0: the last round's counters as they are)
   int update_push = -1;        // the first dense round after a sparse one: its update and its
                                // E pushes in one pass (launch_gossip_update_push) -- -1 when the
                                // round is predicted dense (predict_dense), 0 never, 1 whenever
@@ -429,7 +431,7 @@ bool clearly_sparse(const p2pg_engine* e) {
 // it, never a result.
 bool still_dense(const p2pg_engine* e) {
   double aw = (double)e->prev_aw, av = (double)e->prev_av;
-  if (e->saw_dense && e->last_new < e->prev2_new && e->prev2_aw && e->prev2_av) {
+  if (e->decay_pred && e->saw_dense && e->last_new < e->prev2_new && e->prev2_aw && e->prev2_av) {
     aw *= aw / (double)e->prev2_aw;
     av *= av / (double)e->prev2_av;
   }
@@ -565,6 +567,7 @@ int p2pg_create(const p2pg_config* cfg, p2pg_engine** out) {
   if (const char* f = std::getenv("P2PG_WIDE_ATOMIC")) e->wide_atomic = std::strcmp(f, "0") != 0;
   if (const char* f = std::getenv("P2PG_UPDATE_PUSH")) e->update_push = std::atoi(f);
   if (const char* f = std::getenv("P2PG_RUN_BATCH")) e->batch_rounds = std::atoi(f);
+  if (const char* f = std::getenv("P2PG_DECAY_PRED")) e->decay_pred = std::strcmp(f, "0") != 0;
   if (const char* m = std::getenv("P2PG_GOSSIP_PUSH"))
     e->push_mode = !std::strcmp(m, "atomic") ? 1 : (!std::strcmp(m, "store") ? 2 : 0);
   HIPCHK(e, hipSetDevice(cfg->device));
