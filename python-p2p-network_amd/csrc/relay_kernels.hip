@@ -506,6 +506,106 @@ __global__ __launch_bounds__(256) void k_pull_hub_partial(DevGraph g, DevState s
 
 // Hub targets, part 2: one wave per hub ORs its partial rows, dedups against seen and writes
 // the frontier row; A / S bits by atomicOr (the main pull kernel stored those words whole).
+// The same partial rows with the hub's adjacency segment staged in LDS (north_star: "LDS-staged
+// high-degree adjacency segments"): one 256-thread block per (hub, HUB_CHUNK-slot) item.  All 256
+// threads load the chunk's neighbour ids, activity (and churn) and packed-word masks at once -- one
+// memory trip for the whole segment instead of one per 64-slot window of a single wave -- and
+// compact the active slots into an LDS list (any order: the rows are ORed); then the 4 waves
+// gather the listed rows (lane = word, 8 in flight) and their ORs are folded through LDS.
+// The default since round 4 (A/B against k_pull_hub_partial).
+template <bool CHURN, bool GOSSIP>
+__global__ __launch_bounds__(256) void k_pull_hub_lds(DevGraph g, DevState st, RoundParams p,
+                                                      HubPlan hp) {
+  static_assert(HUB_CHUNK % 256 == 0, "whole slots per thread");
+  __shared__ uint32_t s_row[HUB_CHUNK];   // source row: slot j (gossip, receiver-major E) or v
+  __shared__ uint64_t s_am[HUB_CHUNK];    // its packed-word mask (gossip, packed E)
+  __shared__ uint64_t s_acc[WPB][64];
+  __shared__ uint32_t s_n;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wib = wave_in_block();
+  const int W = st.W;
+  const int prv = (p.round & 1) ^ 1;
+  const uint64_t* __restrict__ Src = GOSSIP ? st.E[prv] : st.F[prv];
+  const uint32_t* __restrict__ Ap = st.A[prv];
+  const uint64_t* __restrict__ AWp = GOSSIP ? st.AW[prv] : nullptr;
+  const bool packed = GOSSIP && AWp != nullptr;
+  const bool valid = lane < W;
+  const uint64_t fm = valid ? full_mask(lane, W, st.M) : 0ull;
+  for (int64_t it = blockIdx.x; it < hp.n_items; it += gridDim.x) {
+    const int64_t item = hp.items[it];
+    const int64_t u = item >> 32;
+    const int64_t chunk = item & 0xFFFFFFFFll;
+    const int64_t rb = g.rowptr[u], re = g.rowptr[u + 1];
+    const int64_t beg = rb + chunk * HUB_CHUNK;
+    const int64_t end = beg + HUB_CHUNK < re ? beg + HUB_CHUNK : re;
+    const uint64_t need = valid ? fm & ~st.seen[u * W + lane] : 0ull;
+    // the same for every wave of the block (same hub): skip a saturated or full hub row
+    const bool run = __ballot(need != 0ull) && !bit_test(st.S, u);
+    if (tid == 0) s_n = 0u;
+    __syncthreads();
+    if (run) {
+#pragma unroll
+      for (int k0 = 0; k0 < HUB_CHUNK; k0 += 256) {
+        const int64_t j = beg + k0 + tid;
+        if (j < end) {
+          const int32_t v = g.colidx[j];
+          bool a = bit_test(Ap, v);
+          if (CHURN && a)
+            a = !churn_dropped((uint32_t)(p.round - 1), gidx(g, u), gidx(g, v), p.churn_thr,
+                               p.cseed_lo, p.cseed_hi);
+          if (a) {
+            const uint32_t at = atomicAdd(&s_n, 1u);
+            s_row[at] = GOSSIP ? (uint32_t)j : (uint32_t)v;
+            s_am[at] = packed ? AWp[v] : 0ull;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    const uint32_t n = s_n;
+    uint64_t acc = 0;
+    for (uint32_t i0 = (uint32_t)wib * 8u; i0 < n; i0 += WPB * 8u) {
+      uint64_t x[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t i = i0 + (uint32_t)k;
+        const bool ok = i < n;
+        x[k] = src_word(Src, ok ? s_row[i] : 0u, W, lane, packed, ok ? s_am[i] : 0ull, ok && need);
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc |= x[k];
+    }
+    s_acc[wib][lane] = acc;
+    __syncthreads();
+    if (wib == 0) {
+      uint64_t r = 0;
+#pragma unroll
+      for (int w = 0; w < WPB; ++w) r |= s_acc[w][lane];
+      hp.partial[it * 64 + lane] = r;
+    }
+    __syncthreads();  // s_n / s_row / s_acc are rewritten by the next item
+  }
+}
+
+// part 1 of the hub pull: the LDS-staged kernel (c4 interleaved A/B, profiles/r04/ab_hub_lds.txt:
+// fused rounds 211.8 -> 210.9 ms per step); P2PG_HUB_LDS=0 keeps one wave per item
+template <bool CHURN, bool GOSSIP>
+void launch_hub_partial(const DevGraph& g, const DevState& st, const RoundParams& p,
+                        const HubPlan& hp, hipStream_t s) {
+  static const bool lds = [] {
+    const char* e = std::getenv("P2PG_HUB_LDS");
+    return !(e && std::strcmp(e, "0") == 0);
+  }();
+  if (lds)
+    hipLaunchKernelGGL((k_pull_hub_lds<CHURN, GOSSIP>),
+                       dim3((unsigned)std::min<int64_t>(hp.n_items, 65535)), dim3(256), 0, s, g, st,
+                       p, hp);
+  else
+    hipLaunchKernelGGL((k_pull_hub_partial<CHURN, GOSSIP>), dim3(grid_tasks(hp.n_items)),
+                       dim3(256), 0, s, g, st, p, hp);
+}
+
 template <bool GOSSIP>
 __global__ __launch_bounds__(256) void k_pull_hub_finalize(DevGraph g, DevState st,
                                                            RoundParams p, HubPlan hp) {
@@ -2198,8 +2298,7 @@ hipError_t pull_with_hubs(const DevGraph& g, const DevState& st, const RoundPara
   if (st.W <= 64) {
     // hubs (deg > HUB_T) are pulled whole in the last phase of a round (phase -1 or 1)
     if (hp.n_items && p.phase != 0)
-      hipLaunchKernelGGL((k_pull_hub_partial<CHURN, GOSSIP>), dim3(grid_tasks(hp.n_items)),
-                         dim3(256), 0, s, g, st, p, hp);
+      launch_hub_partial<CHURN, GOSSIP>(g, st, p, hp, s);
     hipLaunchKernelGGL((k_pull1<CHURN, GOSSIP>),
                        dim3(balanced_grid(k_pull1<CHURN, GOSSIP>, (g.V + 31) >> 5)), dim3(256), 0,
                        s, g, st, p);
@@ -2243,8 +2342,7 @@ hipError_t launch_gossip_pull(const DevGraph& g, const DevState& st, const Round
     pp.store_f = 1;  // the sparse push of this round reads the frontier rows
     // (K = 0: no picks here, and the relay counters take the run's fanout)
     if (hp.n_items)
-      hipLaunchKernelGGL((k_pull_hub_partial<false, true>), dim3(grid_tasks(hp.n_items)),
-                         dim3(256), 0, s, g, st, pp, hp);
+      launch_hub_partial<false, true>(g, st, pp, hp, s);
     if (st.W <= 32)
       hipLaunchKernelGGL((k_gossip_fused<false, 0, 3, true>),
                          dim3(balanced_grid(k_gossip_fused<false, 0, 3, true>, (g.V + 31) >> 5)),
@@ -2262,8 +2360,7 @@ hipError_t launch_gossip_pull(const DevGraph& g, const DevState& st, const Round
   // are left to the hub items as in the fused rounds
   if (grouped_enabled() && grouped_pull_enabled() && st.W <= GROUPED_PULL_W_MAX && p.phase < 0) {
     if (hp.n_items)
-      hipLaunchKernelGGL((k_pull_hub_partial<false, true>), dim3(grid_tasks(hp.n_items)),
-                         dim3(256), 0, s, g, st, p, hp);
+      launch_hub_partial<false, true>(g, st, p, hp, s);
     hipError_t r = launch_gossip_pull_grouped(g, st, p, s);
     if (r != hipSuccess) return r;
     if (hp.n_hubs)
@@ -2485,8 +2582,7 @@ hipError_t launch_gossip_fused(const DevGraph& g, const DevState& st, const Roun
                                bool skip_big, hipStream_t s) {
   if (!gossip_fused_supported(st)) return hipErrorInvalidValue;
   if (hp.n_items)
-    hipLaunchKernelGGL((k_pull_hub_partial<false, true>), dim3(grid_tasks(hp.n_items)),
-                       dim3(256), 0, s, g, st, p, hp);
+    launch_hub_partial<false, true>(g, st, p, hp, s);
   if (grouped_enabled() && st.W <= GROUPED_W_MAX) {
     hipError_t r = launch_gossip_fused_grouped(g, st, p, s);
     if (r != hipSuccess) return r;
