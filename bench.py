@@ -15,7 +15,9 @@ r*4096/N .. (r+1)*4096/N - 1, global message ids, so origins and Philox streams 
 1-GPU run) on a replica of the graph -- strong scaling (fixed total work), no data-path
 collective, because broadcasts are independent bit lanes; value = relays of all ranks /
 max-over-ranks time.  Config 5 (--workload c5) is vertex-partitioned instead (RCCL all-to-all of
-boundary rows), and runs unpartitioned at N = 1.
+boundary rows), and runs unpartitioned at N = 1.  --split vertex / message overrides the
+workload's form (config 4 vertex-partitioned: every rank holds ~5M ghosts of the 10M BA graph at
+N = 8, so the message split stays its default).
 
 Prints ONE JSON line (rank 0) with the driver's fields plus "roofline" (dominant kernel:
 SURVEY.md 8(d)'s algorithmic bytes B_r of the rounds it consumes / its HIP-event time; the
@@ -257,6 +259,9 @@ def main():
                     "(rehearsals only; the reported workload names the size actually run)")
     ap.add_argument("--msgs", type=int, default=0, help="override the workload's broadcast count "
                     "(rehearsals only, e.g. one rank's share of a split; the reported workload names it)")
+    ap.add_argument("--split", default="auto", choices=["auto", "message", "vertex"],
+                    help="multi-GPU form: the workload's own (auto: c5 vertex, else message), the "
+                         "message-axis split, or the 1-D vertex partition")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo stages the exchange through host memory (rehearsal with several "
                          "ranks on one GPU); nccl = RCCL over xGMI")
@@ -298,7 +303,8 @@ def main():
         w["M"] = args.msgs
         w["name"] += f" [REDUCED: {args.msgs} broadcasts]"
     thr = churn_threshold(w.get("churn", 0.0))
-    partitioned = bool(w.get("partition")) and world > 1
+    part_form = bool(w.get("partition")) if args.split == "auto" else args.split == "vertex"
+    partitioned = part_form and world > 1
     t_gen = time.perf_counter()
     g = build_graph(w)
     t_gen = time.perf_counter() - t_gen

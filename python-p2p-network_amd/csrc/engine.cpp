@@ -438,6 +438,15 @@ bool still_dense(const p2pg_engine* e) {
   return av > 0.0 && aw >= e->e_thresh * av * (double)e->W && av >= e->v_thresh * (double)e->v_conn;
 }
 
+// Can this vertex-partitioned rank (global ids set) take the dense rounds (E pushes, fused and
+// pull-only passes in their PART form, relay_kernels.hip)?  Packed rows over 16 < W <= 64 and
+// two E planes; otherwise its gossip pushes go by row atomics only.
+bool part_dense(const p2pg_engine* e) {
+  const DevState& s = e->st;
+  return e->d_gid && e->d_rev && s.E[0] && s.E[1] && s.E[0] != s.E[1] && s.AW[0] &&
+         e->W > GROUPED_W_MAX && e->W <= 64;
+}
+
 // Run this round's update and its (dense) pushes in one pass?
 bool update_push_round(const p2pg_engine* e, const RoundParams& p) {
   if (e->update_push == 0 || e->cfg.mode != P2PG_MODE_GOSSIP || e->push_mode != 0 || e->d_gid ||
@@ -467,6 +476,10 @@ int alloc_edge_planes(p2pg_engine* e) {
   dfree(s.E[0]);
   dfree(s.E[1]);
   if (e->cfg.mode != P2PG_MODE_GOSSIP || !e->d_rev || e->push_mode == 1) return P2PG_OK;
+  // a rank-local graph's ghost slots are usable by the PART kernels only (part_dense)
+  if ((e->cfg.flags & P2PG_FLAG_LOCAL_GRAPH) &&
+      !(e->fused && e->W > GROUPED_W_MAX && e->W <= 64 && s.AW[0]))
+    return P2PG_OK;
   const size_t eb = (size_t)e->nnz * e->W * sizeof(uint64_t);
   size_t free_b = 0, total_b = 0;
   if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || eb + ((size_t)4 << 30) >= free_b)
@@ -616,7 +629,10 @@ int check_csr(p2pg_engine* e, int64_t V, const int64_t* rowptr, const int32_t* c
   }
   // symmetry (every connection relays both ways, node.py:75-78) and reverse slots
   const bool local = (e->cfg.flags & P2PG_FLAG_LOCAL_GRAPH) != 0;
-  rev.assign(e->cfg.mode == P2PG_MODE_GOSSIP && !local && nnz < 0xFFFFFFFFll ? nnz : 0, 0u);
+  // reverse slots for gossip's dense rounds; on a rank-local graph a ghost neighbour's slot is
+  // marked instead (REV_GHOST | its local id), and slot ids must stay below that bit
+  rev.assign(e->cfg.mode == P2PG_MODE_GOSSIP && nnz < (local ? (int64_t)REV_GHOST : 0xFFFFFFFFll) ? nnz : 0,
+             0u);
   int64_t asym = -1;
 #pragma omp parallel for schedule(dynamic, 4096)
   for (int64_t u = 0; u < V; ++u) {
@@ -624,7 +640,10 @@ int check_csr(p2pg_engine* e, int64_t V, const int64_t* rowptr, const int32_t* c
       const int64_t v = colidx[j];
       const int32_t* b = colidx + rowptr[v];
       const int32_t* en = colidx + rowptr[v + 1];
-      if (local && b == en) continue;  // ghost peer: its row lives on its owner rank
+      if (local && b == en) {  // ghost peer: its row lives on its owner rank
+        if (!rev.empty()) rev[j] = REV_GHOST | (uint32_t)v;
+        continue;
+      }
       const int32_t* it = std::lower_bound(b, en, (int32_t)u);
       if (it == en || *it != u) {
 #pragma omp critical
@@ -891,12 +910,17 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
     // predicted dense as well (the previous round's word density; the prediction only picks
     // the push form, never the result), the same pass also pushes this round's receipts.
     const bool dense_pred = e->push_mode == 2 || (e->push_mode == 0 && still_dense(e));
-    fused_round = !e->d_gid && dense_pred && gossip_fused_supported(s);
+    const bool part = e->d_gid != nullptr;  // (a rank gets here only if part_dense)
+    fused_round = (!part || part_dense(e)) && dense_pred && gossip_fused_supported(s);
     if (fused_round) {
       // a frontier nobody observes is not stored: inside p2pg_run (not its last allowed
       // round), without hop/parent records
       p.store_f = (e->skip_frontier && !s.hop) ? 0 : 1;
       if ((rc = timed(e, 7, [&] {
+             if (part) {  // the exchanged row pushes it ORed in are cleared after the pass
+               hipError_t r = launch_gossip_fused(g, s, p, e->hp, nullptr, 0, true, e->stream);
+               return r != hipSuccess ? r : launch_clear_arrivals(s, p.round, e->V, e->stream);
+             }
              const bool wa = wide_atomic_on(e);
              hipError_t r = launch_gossip_fused(g, s, p, e->hp, e->d_hub_big, e->n_hub_big, wa,
                                                 e->stream);
@@ -906,7 +930,11 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
            })))
         return rc;
     } else {
-      if ((rc = timed(e, 5, [&] { return launch_gossip_pull(g, s, p, e->hp, e->stream); }))) return rc;
+      if ((rc = timed(e, 5, [&] {
+             hipError_t r = launch_gossip_pull(g, s, p, e->hp, e->stream);
+             return r != hipSuccess || !part ? r : launch_clear_arrivals(s, p.round, e->V, e->stream);
+           })))
+        return rc;
     }
   } else if (update_push_round(e, p)) {
     // the first dense round after a sparse one: update and E pushes in one pass (timed with the
@@ -955,7 +983,8 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
     // that choice is clear already) and to size the sparse push's (peer, word) list (else
     // bounded by the last round's pushed masks)
     const bool blind = e->round > 0 && e->push_mode != 2 && clearly_sparse(e) && e->prev_sw > 0;
-    if (s.E[0] && !e->d_gid) {  // partitioned gossip pushes by row atomics (ghost rows travel)
+    // (partitioned ranks: E for their local connections when part_dense, ghost rows travel)
+    if (s.E[0] && (!e->d_gid || part_dense(e))) {
       if (e->push_mode == 2) {
         use_e = true;
       } else if (e->push_mode == 0 && !blind) {
@@ -1704,6 +1733,10 @@ int p2pg_snapshot(p2pg_engine* e, void* buf, int64_t cap) {
     return fail(e, P2PG_ERR_STATE, "snapshot: take it before a topology update or after the next round");
   if (!e->frontier_kept)
     return fail(e, P2PG_ERR_STATE, "snapshot: the last round's frontier was not kept");
+  if (e->d_gid && e->cfg.mode == P2PG_MODE_GOSSIP && e->last_push_e && e->round > 0 && !e->done)
+    return fail(e, P2PG_ERR_STATE,
+                "snapshot: a partitioned rank holds this round's pushes per connection; take it "
+                "after a sparse round");
   HIPCHK(e, hipSetDevice(e->cfg.device));
   DevState& s = e->st;
   if (e->cfg.mode == P2PG_MODE_GOSSIP && e->last_push_e && e->round > 0 && !e->done) {

@@ -373,7 +373,21 @@ int p2pg_gossip_targets(uint32_t round, uint32_t peer, uint32_t msg, uint32_t de
     for (uint32_t j = 0; j < deg; ++j) out[j] = j;
     return (int)deg;
   }
-  gossip_picks(round, peer, msg, deg, k, (uint32_t)seed, (uint32_t)(seed >> 32), out);
+  const uint32_t s0 = (uint32_t)seed, s1 = (uint32_t)(seed >> 32);
+  // k <= 4: the folded-round Philox of the device's dense pushes (philox_pick), else the generic
+  if (k <= 4) {
+    const PickKey key = pick_key(round, peer, s0, s1);
+    uint32_t t[4];
+    switch (k) {
+      case 1: { uint32_t o[1]; gossip_picks_k<1>(key, msg, deg, o); t[0] = o[0]; break; }
+      case 2: { uint32_t o[2]; gossip_picks_k<2>(key, msg, deg, o); t[0] = o[0]; t[1] = o[1]; break; }
+      case 3: { uint32_t o[3]; gossip_picks_k<3>(key, msg, deg, o); for (int i = 0; i < 3; ++i) t[i] = o[i]; break; }
+      default: { uint32_t o[4]; gossip_picks_k<4>(key, msg, deg, o); for (int i = 0; i < 4; ++i) t[i] = o[i]; break; }
+    }
+    for (int i = 0; i < k; ++i) out[i] = t[i];
+    return k;
+  }
+  gossip_picks(round, peer, msg, deg, k, s0, s1, out);
   return k;
 }
 

@@ -114,6 +114,92 @@ P2PG_HD void gossip_picks_t(uint32_t round, uint32_t peer, uint32_t msg, uint32_
   }
 }
 
+// The gossip draws of one source (round, peer fixed) for many messages, k <= 4 (one Philox block
+// per message).  In the counter (round, peer, msg, TAG_GSP) only msg varies, so the first two
+// Philox rounds have wave-uniform parts: they are folded into per-source constants once
+// (PickKey, scalar registers on the device), and a message costs 18 multiplies and 19 XORs
+// instead of 20 + 20 and the extra moves of XORs with two scalar operands.  Same outputs as
+// philox4x32_10 (checked against it, tests/test_philox.py and every GPU gossip parity test).
+struct PickKey {
+  uint32_t a1, d2, f2, g3;  // peer ^ k0; hi(M1 z1) ^ k0'; lo(M0 round) ^ k1'; lo(M1 z1) ^ k0''
+  uint32_t k0, k1;          // the key (rounds 3.. use k + i * W)
+};
+
+P2PG_HD PickKey pick_key(uint32_t round, uint32_t peer, uint32_t k0, uint32_t k1) {
+  const uint64_t p0 = (uint64_t)PHILOX_M0 * round;           // round 1, uniform half
+  const uint32_t z1 = (uint32_t)(p0 >> 32) ^ TAG_GSP ^ k1;
+  const uint32_t w1 = (uint32_t)p0;
+  const uint64_t q1 = (uint64_t)PHILOX_M1 * z1;              // round 2, uniform half
+  PickKey k;
+  k.a1 = peer ^ k0;
+  k.d2 = (uint32_t)(q1 >> 32) ^ (k0 + PHILOX_W0);
+  k.f2 = w1 ^ (k1 + PHILOX_W1);
+  k.g3 = (uint32_t)q1 ^ (k0 + 2u * PHILOX_W0);
+  k.k0 = k0;
+  k.k1 = k1;
+  return k;
+}
+
+// philox4x32_10((round, peer, msg, TAG_GSP), k0, k1) for the source of pick_key
+P2PG_HD u32x4 philox_pick(const PickKey& k, uint32_t msg) {
+  // round 1: x = hi(M1 msg) ^ peer ^ k0, y = lo(M1 msg); z, w uniform (in d2 / f2 / g3)
+  uint64_t p1 = (uint64_t)PHILOX_M1 * msg;
+  const uint32_t x1 = (uint32_t)(p1 >> 32) ^ k.a1, y1 = (uint32_t)p1;
+  // round 2: p0 = M0 x1 (per message), p1 = M1 z1 (uniform)
+  uint64_t p0 = (uint64_t)PHILOX_M0 * x1;
+  const uint32_t x2 = y1 ^ k.d2;
+  const uint32_t z2 = (uint32_t)(p0 >> 32) ^ k.f2;
+  const uint32_t w2 = (uint32_t)p0;
+  // round 3: y2 (uniform) is in g3
+  p0 = (uint64_t)PHILOX_M0 * x2;
+  p1 = (uint64_t)PHILOX_M1 * z2;
+  u32x4 c;
+  c.x = (uint32_t)(p1 >> 32) ^ k.g3;
+  c.y = (uint32_t)p1;
+#if defined(__HIP_DEVICE_COMPILE__)
+  c.z = (uint32_t)__builtin_amdgcn_bitop3_b32((uint32_t)(p0 >> 32), w2, k.k1 + 2u * PHILOX_W1, 0x96);
+#else
+  c.z = (uint32_t)(p0 >> 32) ^ w2 ^ (k.k1 + 2u * PHILOX_W1);
+#endif
+  c.w = (uint32_t)p0;
+  uint32_t k0 = k.k0 + 3u * PHILOX_W0, k1 = k.k1 + 3u * PHILOX_W1;
+#pragma unroll
+  for (int i = 3; i < 10; ++i) {
+    p0 = (uint64_t)PHILOX_M0 * c.x;
+    p1 = (uint64_t)PHILOX_M1 * c.z;
+    u32x4 n;
+#if defined(__HIP_DEVICE_COMPILE__)
+    n.x = (uint32_t)__builtin_amdgcn_bitop3_b32((uint32_t)(p1 >> 32), c.y, k0, 0x96);
+    n.z = (uint32_t)__builtin_amdgcn_bitop3_b32((uint32_t)(p0 >> 32), c.w, k1, 0x96);
+#else
+    n.x = (uint32_t)(p1 >> 32) ^ c.y ^ k0;
+    n.z = (uint32_t)(p0 >> 32) ^ c.w ^ k1;
+#endif
+    n.y = (uint32_t)p1;
+    n.w = (uint32_t)p0;
+    c = n;
+    k0 += PHILOX_W0;
+    k1 += PHILOX_W1;
+  }
+  return c;
+}
+
+// gossip_picks_t for one source's PickKey (K <= 4: one Philox block), 32-bit Floyd compares.
+template <int K>
+P2PG_HD void gossip_picks_k(const PickKey& key, uint32_t msg, uint32_t n, uint32_t (&out)[K]) {
+  static_assert(K >= 1 && K <= 4, "one Philox block");
+  const u32x4 r = philox_pick(key, msg);
+#pragma unroll
+  for (int i = 0; i < K; ++i) {
+    const uint32_t jmax = n - (uint32_t)K + (uint32_t)i;
+    const uint32_t t = lemire32(word_of(r, i), jmax + 1u);
+    bool dup = false;
+#pragma unroll
+    for (int q = 0; q < i; ++q) dup |= (out[q] == t);
+    out[i] = dup ? jmax : t;
+  }
+}
+
 // Churn: a send over undirected edge {a,b} made in round r is lost iff the
 // first Philox word is below the threshold floor(p_drop * 2^32).
 P2PG_HD bool churn_dropped(uint32_t round, uint32_t a, uint32_t b, uint32_t threshold,

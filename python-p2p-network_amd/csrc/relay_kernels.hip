@@ -29,6 +29,13 @@
 
 #include "device_util.h"
 
+// Dense pushes: the folded-round Philox of one source's draws (philox_pick); 0 = the generic
+// philox4x32_10 per draw (A/B builds)
+#ifndef P2PG_PICK_FOLD
+#define P2PG_PICK_FOLD 1
+#endif
+
+
 namespace p2pg {
 namespace {
 
@@ -1214,7 +1221,10 @@ __device__ __forceinline__ void tbl_clear(ScatterLds& L, int j, int w) {
 // would make the wave wait (vmcnt) for its own in-flight row stores / atomics.
 // PH: 0 = the whole push; 1 = table + picks only (the flush follows later, PH 2, with the same
 // source, f and receiver slots: the fused kernel defers a short row's flush by one target).
-template <bool CHURN, int K, bool STORE_E, int PH = 0, class CT>
+// PART (vertex-partitioned gossip ranks, STORE_E): a receiver slot marked REV_GHOST is a ghost's
+// connection -- the mask goes into the ghost's row push (next[r+1] row + T bit, exchanged after the
+// round) as in a sparse round, every other one into its E slot.
+template <bool CHURN, int K, bool STORE_E, int PH = 0, bool PART = false, class CT>
 __device__ __forceinline__ void scatter_row(const DevGraph& g, const DevState& st,
                                             const RoundParams& p, ScatterLds& L, int lane,
                                             int64_t v, int64_t rb, int64_t deg, int chunk,
@@ -1235,6 +1245,8 @@ __device__ __forceinline__ void scatter_row(const DevGraph& g, const DevState& s
   const bool anyf = fam != 0ull;
   if (!anyf && !STORE_E) return;
   const uint32_t gv = gidx_s(g, v);
+  // the source's folded Philox rounds (philox_pick: only the message varies per draw)
+  const PickKey pkey = pick_key((uint32_t)p.round, gv, p.gseed_lo, p.gseed_hi);
 
   // Philox + Floyd for list entries [0, n) of this wave, picks ORed into the LDS table.
   auto pick_batch = [&](auto check_v, uint32_t n) {
@@ -1245,8 +1257,11 @@ __device__ __forceinline__ void scatter_row(const DevGraph& g, const DevState& s
       uint32_t* const col = &L.tbl[tbl_entry_ix(e)];  // connection 0's (word, half)
       const uint32_t mb = ok ? 1u << (bit & 31u) : 0u;
       uint32_t pk[K > 0 ? K : 1];
-      gossip_picks_t<(K > 0 ? K : 1)>((uint32_t)p.round, gv, mg, (uint32_t)deg, p.gseed_lo,
-                                      p.gseed_hi, pk);
+      if constexpr (P2PG_PICK_FOLD && K > 0 && K <= 4)
+        gossip_picks_k<K>(pkey, mg, (uint32_t)deg, pk);
+      else
+        gossip_picks_t<(K > 0 ? K : 1)>((uint32_t)p.round, gv, mg, (uint32_t)deg, p.gseed_lo,
+                                        p.gseed_hi, pk);
 #pragma unroll
       for (int q = 0; q < (K > 0 ? K : 1); ++q) {
         const uint32_t jj = pk[q] - (uint32_t)nb;
@@ -1376,10 +1391,10 @@ __device__ __forceinline__ void scatter_row(const DevGraph& g, const DevState& s
       const uint32_t nj = (uint32_t)__builtin_amdgcn_ds_bpermute(
           (nbr0 + (jj < nn ? jj : 0)) << 2, (int)nbr);
       const uint64_t bal = __ballot(ok && x != 0ull);
-      if (STORE_E) {
+      if (STORE_E && !(PART && (nj & REV_GHOST))) {
         if (ok) st_row(&Eo[(int64_t)nj * W + rk_lane], x);
       } else {
-        const int64_t u = (int64_t)nj;
+        const int64_t u = (int64_t)(PART ? nj & ~REV_GHOST : nj);
         if (x) atomicOr((unsigned long long*)&nx[u * W + sl * 64 + wc], (unsigned long long)x);
         if (rk_lane == 0 && ((bal >> (lane & ~(seg - 1))) & segm))
           atomicOr(&Tn[u >> 5], 1u << (u & 31));
@@ -1403,6 +1418,17 @@ __device__ __forceinline__ void scatter_row(const DevGraph& g, const DevState& s
       if (CHURN && bal)
         dropped = churn_dropped((uint32_t)p.round, gv, gidx_s(g, ldc(g.colidx + rb + nb + j)),
                                 p.churn_thr, p.cseed_lo, p.cseed_hi);
+      if (PART && (nj & REV_GHOST)) {  // a ghost's connection: its row push, exchanged
+        const int64_t u = (int64_t)(nj & ~REV_GHOST);
+        if (!dropped && bal) {
+          if (x) atomicOr((unsigned long long*)&nx[u * W + w], (unsigned long long)x);
+          if (lane == 0) {
+            atomicOr(&Tn[u >> 5], 1u << (u & 31));
+            c[ST_SCATTER] += (CT)__popcll(bal);
+          }
+        }
+        continue;
+      }
       // receiver-major: the row lands in the RECEIVER's slot for this connection, so the
       // pull streams its own contiguous slot range; packed: only the active words, in order
       if (st.AW[cur]) {
@@ -1431,7 +1457,7 @@ __device__ __forceinline__ void scatter_row(const DevGraph& g, const DevState& s
 // The scatter launch: tasks [task0, nwords) are 32-peer bitmap words (sources with deg <=
 // GCHUNK), tasks from nwords on are groups of 64 (wide source, chunk) items.  task0 = nwords
 // runs the items only (fused rounds: the items of the pull hubs, deg > HUB_T).
-template <bool CHURN, int K, bool STORE_E>
+template <bool CHURN, int K, bool STORE_E, bool PART = false>
 __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st, RoundParams p,
                                                         const int64_t* __restrict__ hub_items,
                                                         int64_t n_hub, int64_t task0) {
@@ -1489,7 +1515,7 @@ __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st,
           if (lane < W) f2 = Fc[(base + b2) * W + lane];
           rv2 = load_nbr(rb2, (int)deg2);
         }
-        scatter_row<CHURN, K, STORE_E>(g, st, p, L, lane, base + b1, rb1, deg1, 0, 0, f1, rv1, 0,
+        scatter_row<CHURN, K, STORE_E, 0, PART>(g, st, p, L, lane, base + b1, rb1, deg1, 0, 0, f1, rv1, 0,
                                        c PROF_PASS);
         b1 = b2;
         rb1 = rb2;
@@ -1526,7 +1552,7 @@ __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st,
       for (int sl = 0; sl < nslices; ++sl) {
         const int w = sl * 64 + lane;
         const uint64_t f = w < W ? Fc[v * W + w] : 0ull;
-        scatter_row<CHURN, K, STORE_E>(g, st, p, L, lane, v, rb, deg, chunk, sl, f, rv, 0, c PROF_PASS);
+        scatter_row<CHURN, K, STORE_E, 0, PART>(g, st, p, L, lane, v, rb, deg, chunk, sl, f, rv, 0, c PROF_PASS);
       }
     };
     if (task < nwords) {  // multi-slice rows (W > 64)
@@ -1594,14 +1620,19 @@ constexpr int FG = P2PG_FG;
 // row atomics afterwards); the software pipeline runs across task boundaries, which k_pull1's
 // per-task three-stage pipeline does not.
 // HALF (MODE 0, W <= 32): arrivals gathered two slots per load (src_word_pair).
-template <bool CHURN, int K, int MODE = 0, bool HALF = false>
+// PART (vertex-partitioned gossip ranks, 16 < W <= 64): no E slot of a ghost neighbour is gathered
+// (REV_GHOST in rev; its sends arrive as exchanged row pushes, next[r&1] + T bits, ORed into the
+// arrivals here), pushes to ghosts go to their row pushes (scatter_row PART), Philox ids are
+// global (gid).  The caller clears the consumed row pushes afterwards (launch_clear_arrivals).
+template <bool CHURN, int K, int MODE = 0, bool HALF = false, bool PART = false>
 __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph g, DevState st,
                                                                         RoundParams p) {
   constexpr bool PO = MODE == 1, UP = MODE == 2, PL = MODE == 3;
   constexpr bool GATHER = MODE == 0 || PL;  // arrivals gathered from E
-  // never partitioned (local ids are the Philox ids) and never on a pre-update graph: known here,
+  static_assert(!(PART && UP), "no update+push pass on partitioned ranks");
+  // (not partitioned: local ids are the Philox ids) and never on a pre-update graph: known here,
   // so the id translation and lost-slot tests fold away (fewer live scalar registers)
-  g.gid = nullptr;
+  if (!PART) g.gid = nullptr;
   g.gone = nullptr;
   g.gdeg = g.gpos = nullptr;
   __shared__ ScatterLds lds[WPB];
@@ -1689,7 +1720,7 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
     const uint32_t j = q.beg + lane;
     if (j < q.end) {
       if (GATHER) q.v = ld_once(&g.colidx[j]);
-      if (!PL) q.rv = ld_once(&g.rev[j]);
+      if (!PL || PART) q.rv = ld_once(&g.rev[j]);  // (PART: ghost marks)
     }
   };
   // loads only; gather() tests the bit (see k_pull1)
@@ -1716,7 +1747,8 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
     }
     const uint64_t needm = __ballot((fm & ~q.s) != 0ull);
     const uint32_t jq = q.beg + lane;
-    uint64_t m = __ballot(jq < q.end && ((q.aword >> (q.v & 31)) & 1u));
+    uint64_t m = __ballot(jq < q.end && ((q.aword >> (q.v & 31)) & 1u) &&
+                          !(PART && (q.rv & REV_GHOST)));
     if constexpr (HALF) {  // FG slots in flight, two per load (FG / 2 loads)
       constexpr int FH = FG / 2;
       uint32_t r0[FH], r1[FH], m0[FH], m1[FH];
@@ -1813,7 +1845,7 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
   uint32_t prcv = 0;  // its receiver slots
   auto flush_pending = [&]() {
     if (pend) {
-      scatter_row<CHURN, K, true, 2>(g, st, p, lds[wib], lane, pu, pbeg, pdeg, 0, 0, pnw, prcv,
+      scatter_row<CHURN, K, true, 2, PART>(g, st, p, lds[wib], lane, pu, pbeg, pdeg, 0, 0, pnw, prcv,
                                      0, c PROF_PASS);
       pend = false;
     }
@@ -1841,6 +1873,11 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
 #pragma unroll
     for (int k = 0; k < FG; ++k) acc |= X[k];
     if (UP) acc = a.am;  // the push row
+    // PART: the rows other ranks pushed to u in the last round (exchanged; T bit), loaded now so
+    // the wait below covers them
+    uint64_t remote = 0;
+    if (PART && GATHER && ((ldc(st.T[cur] + (u >> 5)) >> (u & 31)) & 1u) && valid)
+      remote = ld_once(&st.next[cur][(int64_t)u * W + lane]);
     PROF_MARK(0);
     if (GATHER) {
       uint64_t m = a.mr;  // the rest of the first 64 slots, then further 64-slot chunks
@@ -1904,7 +1941,7 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
         sam = 0;
         if (j < a.end) {
           const int32_t v = g.colidx[j];
-          act = bit_test(Ap, v);
+          act = bit_test(Ap, v) && !(PART && (g.rev[j] & REV_GHOST));
           if (act) sam = AWp[v];
         }
         m = __ballot(act);
@@ -1918,6 +1955,7 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     PROF_MARK(1);
     if (HALF) acc |= bperm64(lane ^ 32, acc);  // lanes 32-63 gathered for words 0-31 too
+    if (PART) acc |= remote;
     if (UP && acc) {  // the push row is consumed: all-zero again outside touched rows
       st_prow(&st.next[cur][(int64_t)u * W + lane], 0ull);
       c[ST_AUX] += 1;  // touched (pushed-to) words consumed
@@ -1959,7 +1997,7 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
       if (PL) {
         // (no pushes: the sparse push that follows reads the frontier row)
       } else if (deg <= (uint64_t)GCHUNK) {
-        scatter_row<CHURN, K, true, 1>(g, st, p, lds[wib], lane, u, a.beg, (int64_t)deg, 0, 0,
+        scatter_row<CHURN, K, true, 1, PART>(g, st, p, lds[wib], lane, u, a.beg, (int64_t)deg, 0, 0,
                                        nw, a.rv, 0, c PROF_PASS);
         pend = true;
         pu = u;
@@ -1969,7 +2007,7 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
         prcv = a.rv;
       } else if (deg <= 64) {
         for (int ch = 0; (int64_t)ch * GCHUNK < (int64_t)deg; ++ch)
-          scatter_row<CHURN, K, true>(g, st, p, lds[wib], lane, u, a.beg, (int64_t)deg, ch, 0,
+          scatter_row<CHURN, K, true, 0, PART>(g, st, p, lds[wib], lane, u, a.beg, (int64_t)deg, ch, 0,
                                       nw, a.rv, ch * GCHUNK, c PROF_PASS);
       } else {
         for (int ch = 0; (int64_t)ch * GCHUNK < (int64_t)deg; ++ch) {
@@ -1977,7 +2015,7 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
           const uint32_t j = a.beg + (uint32_t)(ch * GCHUNK - off) + lane;
           const uint32_t rvb = j < a.end ? g.rev[j] : 0u;
           __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-          scatter_row<CHURN, K, true>(g, st, p, lds[wib], lane, u, a.beg, (int64_t)deg, ch, 0,
+          scatter_row<CHURN, K, true, 0, PART>(g, st, p, lds[wib], lane, u, a.beg, (int64_t)deg, ch, 0,
                                       nw, rvb, off, c PROF_PASS);
         }
       }
@@ -2319,6 +2357,71 @@ hipError_t launch_flood_pull(const DevGraph& g, const DevState& st, const RoundP
                      : pull_with_hubs<false, false>(g, st, p, hp, s);
 }
 
+// k_gossip_fused by churn / fanout (MODE 0, PART) and width (HALF: W <= 32)
+template <bool CH, int KK, int MODE, bool PART>
+static void fused_launch(bool half, const DevGraph& g, const DevState& st, const RoundParams& p,
+                         hipStream_t s) {
+  if (half)
+    hipLaunchKernelGGL((k_gossip_fused<CH, KK, MODE, true, PART>),
+                       dim3(balanced_grid(k_gossip_fused<CH, KK, MODE, true, PART>, (g.V + 31) >> 5)),
+                       dim3(256), 0, s, g, st, p);
+  else
+    hipLaunchKernelGGL((k_gossip_fused<CH, KK, MODE, false, PART>),
+                       dim3(balanced_grid(k_gossip_fused<CH, KK, MODE, false, PART>, (g.V + 31) >> 5)),
+                       dim3(256), 0, s, g, st, p);
+}
+
+// Partitioned ranks (PART, see internal.h): no hub split (H = nullptr: every peer, hubs included,
+// goes through the fused pipeline, whose wide-row chunks handle any degree).
+static bool part_launch_ok(const DevGraph& g, const DevState& st, int prv) {
+  return g.gid != nullptr && g.rev != nullptr && st.W > GROUPED_W_MAX && st.W <= 64 &&
+         st.AW[prv] != nullptr && st.E[0] != st.E[1];
+}
+
+static hipError_t launch_gossip_fused_part(const DevGraph& g, const DevState& st,
+                                           const RoundParams& p, hipStream_t s) {
+  if (!part_launch_ok(g, st, (p.round & 1) ^ 1) || p.phase >= 0) return hipErrorInvalidValue;
+  DevGraph g2 = g;
+  g2.H = nullptr;
+  const bool half = st.W <= 32;
+  const bool ch = p.churn_thr != 0;
+  switch (p.fanout) {
+    case 1: ch ? fused_launch<true, 1, 0, true>(half, g2, st, p, s) : fused_launch<false, 1, 0, true>(half, g2, st, p, s); break;
+    case 2: ch ? fused_launch<true, 2, 0, true>(half, g2, st, p, s) : fused_launch<false, 2, 0, true>(half, g2, st, p, s); break;
+    case 3: ch ? fused_launch<true, 3, 0, true>(half, g2, st, p, s) : fused_launch<false, 3, 0, true>(half, g2, st, p, s); break;
+    case 4: ch ? fused_launch<true, 4, 0, true>(half, g2, st, p, s) : fused_launch<false, 4, 0, true>(half, g2, st, p, s); break;
+    default: ch ? fused_launch<true, 0, 0, true>(half, g2, st, p, s) : fused_launch<false, 0, 0, true>(half, g2, st, p, s); break;
+  }
+  return hipGetLastError();
+}
+
+// After a PART gather round: the exchanged row pushes it consumed (next[r&1] rows with a T bit,
+// saturated peers' included) are cleared, so the plane is all-zero outside pending pushes again.
+// One wave per 64 bitmap words (lane = word), then lane = row word per set bit.
+__global__ __launch_bounds__(256) void k_clear_arrivals(DevState st, int32_t round, int64_t nwords) {
+  const int lane = threadIdx.x & 63;
+  const int W = st.W;
+  const int cur = round & 1;
+  uint32_t* __restrict__ T = st.T[cur];
+  uint64_t* __restrict__ nx = st.next[cur];
+  for (int64_t base = ((int64_t)blockIdx.x * WPB + wave_in_block()) * 64; base < nwords;
+       base += (int64_t)gridDim.x * WPB * 64) {
+    const int64_t i = base + lane;
+    const uint32_t t = i < nwords ? T[i] : 0u;
+    if (t) T[i] = 0u;
+    for (uint64_t m = __ballot(t != 0u); m; m &= m - 1ull) {
+      const int l = __builtin_ctzll(m);
+      uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)t, l);
+      const int64_t w0 = (base + l) << 5;
+      while (b) {
+        const int64_t u = w0 + __builtin_ctz(b);
+        b &= b - 1u;
+        if (lane < W) nx[u * W + lane] = 0ull;
+      }
+    }
+  }
+}
+
 static bool grouped_enabled();
 static bool grouped_pull_enabled() {
   static const bool on = [] {
@@ -2337,6 +2440,15 @@ hipError_t launch_gossip_pull(const DevGraph& g, const DevState& st, const Round
     const char* e = std::getenv("P2PG_FUSED_PULL");
     return !(e && std::strcmp(e, "0") == 0);
   }();
+  if (g.gid && p.phase < 0) {  // partitioned ranks: the PART pull-only pass, hubs inline
+    if (!part_launch_ok(g, st, (p.round & 1) ^ 1)) return hipErrorInvalidValue;
+    DevGraph g2 = g;
+    g2.H = nullptr;
+    RoundParams pp = p;
+    pp.store_f = 1;
+    fused_launch<false, 0, 3, true>(st.W <= 32, g2, st, pp, s);
+    return hipGetLastError();
+  }
   if (fused_pull && st.W <= 64 && st.AW[(p.round & 1) ^ 1] && p.phase < 0) {
     RoundParams pp = p;
     pp.store_f = 1;  // the sparse push of this round reads the frontier rows
@@ -2444,9 +2556,17 @@ template <bool SE>
 void scatter_dispatch(int grid, const DevGraph& g, const DevState& st, const RoundParams& p,
                       const int64_t* hub_items, int64_t n_hub_items, int64_t task0,
                       hipStream_t s) {
-#define P2PG_SCATTER(CH, KK)                                                                 \
-  hipLaunchKernelGGL((k_gossip_scatter<CH, KK, SE>), dim3(grid), dim3(256), 0, s, g, st, p,  \
-                     hub_items, n_hub_items, task0)
+  // (partitioned ranks' E stores: ghost connections go to row pushes, scatter_row PART)
+  const bool part = SE && g.gid != nullptr;
+#define P2PG_SCATTER(CH, KK)                                                                   \
+  do {                                                                                         \
+    if (part)                                                                                  \
+      hipLaunchKernelGGL((k_gossip_scatter<CH, KK, SE, true>), dim3(grid), dim3(256), 0, s, g, \
+                         st, p, hub_items, n_hub_items, task0);                                \
+    else                                                                                       \
+      hipLaunchKernelGGL((k_gossip_scatter<CH, KK, SE>), dim3(grid), dim3(256), 0, s, g, st,   \
+                         p, hub_items, n_hub_items, task0);                                    \
+  } while (0)
   const bool ch = p.churn_thr != 0;
   switch (p.fanout) {
     case 1: if (ch) P2PG_SCATTER(true, 1); else P2PG_SCATTER(false, 1); break;
@@ -2486,7 +2606,7 @@ hipError_t launch_gossip_scatter(const DevGraph& g, const DevState& st, const Ro
     return !(e && std::strcmp(e, "0") == 0);
   }();
   const bool hubs_ok = hub_pushes_ready(g, big_items, n_big, wide_big, n_wide_big);
-  if (store_e && push_grouped && grouped_enabled() && st.W <= GROUPED_W_MAX && hubs_ok) {
+  if (store_e && push_grouped && grouped_enabled() && st.W <= GROUPED_W_MAX && hubs_ok && !g.gid) {
     hipError_t r = launch_gossip_push_grouped(g, st, p, s);
     if (r != hipSuccess) return r;
     return launch_wide_push_e(g, st, p, big_items, n_big, wide_big, n_wide_big, s);
@@ -2496,7 +2616,7 @@ hipError_t launch_gossip_scatter(const DevGraph& g, const DevState& st, const Ro
     const char* e = std::getenv("P2PG_PUSH_FUSED");
     return !(e && std::strcmp(e, "0") == 0);
   }();
-  if (store_e && push_fused && st.W <= 64 && st.AW[p.round & 1] != nullptr && hubs_ok) {
+  if (store_e && push_fused && st.W <= 64 && st.AW[p.round & 1] != nullptr && hubs_ok && !g.gid) {
 #define P2PG_FUSED_PO(CH, KK)                                                                       \
   hipLaunchKernelGGL((k_gossip_fused<CH, KK, 1>),                                                 \
                      dim3(balanced_grid(k_gossip_fused<CH, KK, 1>, (g.V + 31) >> 5)), dim3(256),    \
@@ -2581,6 +2701,7 @@ hipError_t launch_gossip_fused(const DevGraph& g, const DevState& st, const Roun
                                const HubPlan& hp, const int64_t* big_items, int64_t n_big,
                                bool skip_big, hipStream_t s) {
   if (!gossip_fused_supported(st)) return hipErrorInvalidValue;
+  if (g.gid) return launch_gossip_fused_part(g, st, p, s);  // (the caller clears the arrivals)
   if (hp.n_items)
     launch_hub_partial<false, true>(g, st, p, hp, s);
   if (grouped_enabled() && st.W <= GROUPED_W_MAX) {
@@ -2621,6 +2742,13 @@ hipError_t launch_gossip_fused(const DevGraph& g, const DevState& st, const Roun
     const int64_t nwords = (g.V + 31) >> 5;
     scatter_dispatch<true>(grid_tasks((n_big + 63) >> 6), g, st, p, big_items, n_big, nwords, s);
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_clear_arrivals(const DevState& st, int32_t round, int64_t V, hipStream_t s) {
+  const int64_t nwords = (V + 31) >> 5;
+  hipLaunchKernelGGL(k_clear_arrivals, dim3(grid_tasks((nwords + 63) >> 6)), dim3(256), 0, s, st,
+                     round, nwords);
   return hipGetLastError();
 }
 

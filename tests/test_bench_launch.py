@@ -87,3 +87,26 @@ def test_bench_c5_partitioned_8_ranks_gloo():
     assert j8["relays_per_step"] == j1["relays_per_step"]
     assert j8["config"]["rounds"] == j1["config"]["rounds"]
     assert 0.0 < j8["exchange_live_row_frac"] <= 1.0
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+def test_bench_c4_vertex_split_4_ranks_gloo():
+    """Config 4's gossip as a 1-D vertex partition (`--split vertex`) at 4 ranks (gloo, cuda:0)
+    on a 1M-peer BA graph, W = 64: the ranks run the dense rounds in their partitioned form (E
+    planes for local connections, ghost pushes exchanged) and the JSON line reports the 1-GPU
+    run's relays and rounds."""
+    common = ["--workload", "c4", "--peers", "1000000", "--steps", "1", "--warmup", "0",
+              "--no-cpu-baseline"]
+    one = _bench(["--gpus", "1", *common], _env(), timeout=300)
+    assert one.returncode == 0, one.stderr[-4000:]
+    j1 = _json_line(one.stdout)
+    four = _bench(["--gpus", "4", "--split", "vertex", "--dist-backend", "gloo", *common], _env(),
+                  timeout=600)
+    assert four.returncode == 0, four.stderr[-4000:]
+    j4 = _json_line(four.stdout)
+    assert j4["n_gpus"] == 4
+    assert "vertex partition x4" in j4["config"]["parallelism"]
+    assert j4["relays_per_step"] == j1["relays_per_step"]
+    assert j4["config"]["rounds"] == j1["config"]["rounds"]
+    assert j4["kernel_ms_per_step"].get("gossip_fused", 0.0) > 0.0  # dense rounds on the ranks

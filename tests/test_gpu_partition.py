@@ -52,10 +52,13 @@ class ThreadTransport:
         self.s["barrier"].wait()  # every rank has copied out of the send buffers
 
 
-def run_partitioned(g, world, src, overlap=True, **kw):
+def run_partitioned(g, world, src, overlap=True, forms=None, **kw):
+    """forms: a list that receives each rank's local push forms (round stats' push_form)."""
     from p2pnetwork.gpu import PartitionedNetwork
     shared = {"slots": [None] * world, "barrier": threading.Barrier(world)}
     results, errors = [None] * world, []
+    if forms is not None:
+        forms[:] = [None] * world
 
     def rank_main(rank):
         try:
@@ -66,6 +69,8 @@ def run_partitioned(g, world, src, overlap=True, **kw):
                 gids, seen = net.owned_planes()
                 hp = net.owned_hop_parent() if kw.get("record") else None
             results[rank] = (rounds, gids, seen, hp)
+            if forms is not None:
+                forms[rank] = [r.push_form for r in net.local_rounds]
         except BaseException as exc:  # surface in the main thread; unblock the others
             errors.append(exc)
             shared["barrier"].abort()
@@ -139,6 +144,49 @@ def test_partitioned_engines_match_single_gpu(kind, mode, M, thr, world, overlap
     np.testing.assert_array_equal(par, par1)
     # and the single engine against the oracle (C restatement)
     ora = coracle.run(g.rowptr, g.colidx, src, mode, 3, 99, 0, thr, 17, record=True)
+    np.testing.assert_array_equal(hop1, ora.hop)
+    np.testing.assert_array_equal(par1, ora.parent)
+
+
+# Partitioned ranks take gossip's dense rounds at 16 < W <= 64 (relay_kernels.hip PART kernels):
+# E planes for local connections, row pushes for ghost connections (exchanged as plane 1) ORed
+# into the gather of the next round.  Widths 24 / 32 (two slots per gather load) / 64, the engine's
+# own schedule and every round forced dense (P2PG_GOSSIP_PUSH=store), churn, hubs on one rank,
+# records (hop / parent, ghost senders): == one engine == the C oracle.
+@pytest.mark.parametrize("kind,M,world,thr,env", [
+    ("ba", 1536, 3, 300_000_000, {"P2PG_GOSSIP_PUSH": "store"}),
+    ("ba", 2048, 2, 0, {"P2PG_V_THRESH": "0.2"}),
+    ("ws", 4096, 4, 200_000_000, {"P2PG_V_THRESH": "0.2"}),
+    ("ws", 1100, 3, 0, {"P2PG_GOSSIP_PUSH": "store"}),
+])
+def test_partitioned_gossip_dense_rounds(kind, M, world, thr, env, monkeypatch):
+    from p2pnetwork.gpu import GraphNetwork, make_sources
+    from p2pnetwork.gpu.network import PUSH_FORMS
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    g = graph(kind)
+    src = make_sources(g.V, M, seed=31)
+    kw = dict(mode="gossip", fanout=3, gossip_seed=77, churn_threshold_value=thr, churn_seed=23)
+    forms = []
+    res = run_partitioned(g, world, src, overlap=True, forms=forms, record=True, **kw)
+    dense = {PUSH_FORMS.index("edge"), PUSH_FORMS.index("fused")}
+    assert all(any(f in dense for f in fr) for fr in forms), forms
+    assert any(PUSH_FORMS.index("fused") in fr for fr in forms), forms
+    with GraphNetwork(g, record=True, **kw) as one:
+        one.broadcast(src)
+        rounds1 = one.run()
+        seen1 = one.seen_plane()
+        hop1, par1 = one.hop_parent()
+    np.testing.assert_array_equal(assemble(res, g.V, (M + 63) // 64), seen1)
+    for rounds, *_ in res:
+        _assert_same_rounds(rounds, rounds1)
+    hop = np.full((g.V, M), -1, np.int32)
+    par = np.full((g.V, M), -1, np.int32)
+    for _, _, _, (gids, h, p) in res:
+        hop[gids], par[gids] = h, p
+    np.testing.assert_array_equal(hop, hop1)
+    np.testing.assert_array_equal(par, par1)
+    ora = coracle.run(g.rowptr, g.colidx, src, "gossip", 3, 77, 0, thr, 23, record=True)
     np.testing.assert_array_equal(hop1, ora.hop)
     np.testing.assert_array_equal(par1, ora.parent)
 
@@ -273,7 +321,7 @@ def test_partitioned_8_ranks_full_width_flood_churn():
 
 def test_partitioned_8_ranks_full_width_gossip():
     """Gossip (k = 3, churn 0.05) over 8 ranks at W = 64 on a 1M-peer BA graph (hubs at the low
-    ids, on rank 0): the assembled seen plane and the global per-round counters == one engine;
+    ids, on rank 0; every rank runs fused dense rounds): the assembled seen plane and the global per-round counters == one engine;
     words 0 and 63 == the C oracle's delivered sets (their broadcasts run alone, with their global
     message ids)."""
     from p2pnetwork.gpu import GraphNetwork, PeerGraph, make_sources
@@ -283,7 +331,11 @@ def test_partitioned_8_ranks_full_width_gossip():
     M, world = 4096, 8
     src = make_sources(g.V, M, seed=1)
     kw = dict(mode="gossip", fanout=3, gossip_seed=0x5EED, churn_threshold_value=thr, churn_seed=0xC0FFEE)
-    res = run_partitioned(g, world, src, overlap=True, **kw)
+    forms = []
+    res = run_partitioned(g, world, src, overlap=True, forms=forms, **kw)
+    # the dense rounds run on the ranks too (PART kernels), not row atomics only
+    from p2pnetwork.gpu.network import PUSH_FORMS
+    assert all(PUSH_FORMS.index("fused") in fr for fr in forms), forms
     with GraphNetwork(g, **kw) as one:
         one.broadcast(src)
         rounds1 = one.run()

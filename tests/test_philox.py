@@ -54,3 +54,25 @@ def test_sources_library_matches_oracle():
     from p2pnetwork.gpu import make_sources
     for V, M, seed, base in [(1000, 64, 1, 0), (10_000_000, 4096, 7, 4096), (3, 10, 2**40 + 5, 9)]:
         assert np.array_equal(make_sources(V, M, seed, base), philox.make_sources(V, M, seed, base))
+
+
+@pytest.mark.parametrize("k", [1, 2, 3, 4, 5, 7])
+def test_library_gossip_targets_match_oracle(k):
+    """p2pg_gossip_targets (the host twin of the device pushes; k <= 4 through the folded-round
+    Philox of philox_pick / gossip_picks_k, which the dense pushes use) == the oracle's picks."""
+    import ctypes
+    from p2pnetwork.gpu import _lib
+    rng = np.random.default_rng(k)
+    n = 300
+    rnd = rng.integers(0, 60, n)
+    peer = rng.integers(0, 2**32, n, dtype=np.uint64)
+    msg = rng.integers(0, 2**32, n, dtype=np.uint64)
+    deg = rng.integers(k + 1, 20000, n)
+    seed = int(rng.integers(0, 2**63))
+    want = philox.gossip_picks(rnd, peer, msg, deg, k, seed)
+    out = np.zeros(16, dtype=np.uint32)
+    for i in range(n):
+        got = _lib.lib().p2pg_gossip_targets(int(rnd[i]), int(peer[i]), int(msg[i]), int(deg[i]), k,
+                                             seed, out.ctypes.data_as(ctypes.c_void_p))
+        assert got == k
+        assert out[:k].tolist() == [int(x) for x in want[i]], i
