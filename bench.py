@@ -381,6 +381,19 @@ def main():
     achieved = sb_dom / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
     achieved_engine = mb[dominant] / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
     kernel_ms_total = sum(v[0] for v in kt.values())
+    by_round = None
+    if w["mode"] == "gossip" and world == 1:
+        # untimed: one more broadcast stepped round by round, the dominant kernel's device time
+        # per round (a change of the dense-round schedule cannot pass for kernel speed); stepping
+        # stores every round's frontier, which p2pg_run skips where nobody reads it
+        net.reset()
+        by_round = []
+        while True:
+            k0 = net.kernel_times()[dominant][0]
+            st = net.step()
+            by_round.append(round(net.kernel_times()[dominant][0] - k0, 3))
+            if not st.active:
+                break
     out = {
         "metric": "msg-edge relays/sec (GTEPS) at 10M peers x 4096 msgs; % HBM roofline",
         "value": relays / elapsed / 1e9,
@@ -419,6 +432,7 @@ def main():
             "engine_model_bytes_per_launch": mb[dominant] / max(dom_n, 1),
         },
         "kernel_ms_per_step": {k: v[0] for k, v in kt.items()},
+        "dominant_ms_by_round": by_round,
         "model_bytes_per_step": mb,
         "whole_step_model_GBps": sum(mb.values()) / (elapsed / args.steps) / 1e9,
         "survey_model_bytes_per_step": sb_step,
