@@ -2,6 +2,7 @@
 reference's own Node objects and against the CPU oracle -- bit-exact hop, parent, delivered
 set, per-round relays and byte-model counters; plus size-independent properties at the
 BASELINE.json full sizes (config 3 flood, config 4 gossip)."""
+import os
 import zlib
 
 import numpy as np
@@ -281,6 +282,31 @@ def test_config4_full_size_counters_are_the_sum_of_its_words(c4_full):
         np.testing.assert_array_equal(col, seen[:, w], err_msg=f"word {w}")
         for i, r in enumerate(sub):
             tot[i] += [getattr(r, k) for k in keys]
+    for j, k in enumerate(keys):
+        np.testing.assert_array_equal(trim_zeros(tot[:, j]), trim_zeros([getattr(r, k) for r in a]),
+                                      err_msg=k)
+
+
+@pytest.mark.skipif(not os.environ.get("P2PG_FULL_ORACLE"),
+                    reason="whole-plane oracle pin of config 4 (~7 min of C oracle): P2PG_FULL_ORACLE=1")
+@pytest.mark.timeout(1500)
+def test_config4_full_size_every_word_matches_c_oracle(c4_full):
+    """All 64 words of config 4's 4096-broadcast seen plane == the C oracle's 64-broadcast runs
+    of their messages (seen sets, 10M peers each), and the 4096-run's additive per-round counters
+    (first receipts, relays, active words, wedges, pushed masks) == the sum of the 64 oracle runs'
+    -- the whole plane pinned to the oracle, not only the C4_WORDS below."""
+    from oracle import coracle
+    g, src, seen, a, _ = c4_full
+    keys = ("new_deliveries", "relays", "active_words", "wedges", "scatter_words")
+    tot = np.zeros((len(a) + 8, len(keys)), dtype=np.int64)
+    for w in range(64):
+        base = 64 * w
+        ora = coracle.run(g.rowptr, g.colidx, src[base:base + 64], "gossip", 3, 0x5EED,
+                          msg_id_base=base, record=False, want_seen=True)
+        np.testing.assert_array_equal(ora.seen[:, 0], seen[:, w], err_msg=f"word {w}")
+        for i, r in enumerate(ora.rounds):
+            tot[i] += [r[k] for k in keys]
+        print(f"word {w}: {len(ora.rounds)} rounds, equal", flush=True)
     for j, k in enumerate(keys):
         np.testing.assert_array_equal(trim_zeros(tot[:, j]), trim_zeros([getattr(r, k) for r in a]),
                                       err_msg=k)
