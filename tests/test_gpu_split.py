@@ -68,7 +68,10 @@ def test_message_split_union_with_churn_and_ragged_words():
                  bounds=[0, 1024, 1984, 2129])
 
 
-def test_message_split_config4_full_size_8_ranks():
-    """Config 4 itself (10M-peer BA m=4, 4096 gossips, k=3) as the 8-GPU job runs it."""
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_message_split_config4_full_size(world):
+    """Config 4 itself (10M-peer BA m=4, 4096 gossips, k=3) as the 2- / 4- / 8-GPU jobs run it:
+    the W = 32 / 16 / 8 shares (HALF-mode fused kernel, grouped kernels) union to the one-engine
+    run, word for word and counter for counter."""
     from p2pnetwork.gpu import PeerGraph
-    _check_split(PeerGraph.barabasi_albert(10_000_000, 4, seed=1), 4096, 8)
+    _check_split(PeerGraph.barabasi_albert(10_000_000, 4, seed=1), 4096, world)
