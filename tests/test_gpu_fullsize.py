@@ -12,6 +12,8 @@
   packed-E / fused / compact-flush paths): the whole seen plane and every per-round counter ==
   the C oracle, in every push form.
 Each test prints nothing for up to ~2 minutes (graph generation and the CPU oracle)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -69,6 +71,35 @@ def test_config5_full_size_flood_churn(config5):
                       churn_seed=CSEED, record=False, want_seen=True)
     np.testing.assert_array_equal(ora.seen[:, 0], cols[63])
     assert_rounds_equal(rounds, ora.rounds)
+
+
+def _c5_word_range():
+    r = os.environ.get("P2PG_C5_WORDS", "")
+    if not r:
+        return None
+    lo, hi = (int(x) for x in r.split("-"))
+    return range(lo, hi + 1)
+
+
+@pytest.mark.skipif(_c5_word_range() is None,
+                    reason="config 5 seen plane vs the C oracle, words lo..hi (~25 s each): P2PG_C5_WORDS=lo-hi")
+@pytest.mark.timeout(1500)
+def test_config5_full_size_words_match_c_oracle(config5):
+    """Words lo..hi of config 5's 4096-flood seen plane (100M peers, churn 0.05) == the C
+    oracle's 64-flood runs of their messages, whose every churn decision it re-draws; run in
+    ranges (P2PG_C5_WORDS) so that the 64 words fit the box's time limit per call."""
+    g, src, thr = config5
+    words = _c5_word_range()
+    with c5_net(g, thr) as net:
+        net.broadcast(src)
+        net.run()
+        cols = {w: net.seen_word(w) for w in words}
+    for w in words:
+        ora = coracle.run(g.rowptr, g.colidx, src[64 * w:64 * (w + 1)], "flood", churn_threshold=thr,
+                          churn_seed=CSEED, record=False, want_seen=True)
+        assert np.array_equal(cols.pop(w), ora.seen[:, 0]), f"word {w}"
+        print(f"word {w}: {len(ora.rounds)} rounds, equal", flush=True)
+        del ora
 
 
 def test_config5_word0_hop_parent_match_c_oracle(config5):
