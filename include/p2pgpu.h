@@ -59,8 +59,10 @@ extern "C" {
                                     round (the caller decides global quiescence)          */
 #define P2PG_FLAG_LOCAL_GRAPH 8u /* rank-local graph of a vertex partition: ghost peers have
                                     empty rows, so symmetry is checked between non-empty
-                                    rows only; gossip pushes use row atomics (no reverse
-                                    slots, no per-connection push plane)                   */
+                                    rows only; a ghost's reverse slot is marked, so at
+                                    16 < W <= 64 gossip takes the dense rounds (per-
+                                    connection pushes for local connections, row pushes for
+                                    ghost ones, exchanged); narrower rows: row atomics only */
 
 typedef struct p2pg_engine p2pg_engine;
 typedef struct p2pg_graph p2pg_graph;
