@@ -1602,8 +1602,13 @@ constexpr int FG = P2PG_FG;
 // no second pass over the peers), and the Philox work of one target overlaps the first
 // gathers of the next target, which are already in flight.  Hubs (deg > HUB_T) are pulled by k_pull_hub_*
 // and pushed by a chunk-item scatter launch over the hubs only.
+// Waves per SIMD the launch bounds ask for.  Both 3 and 4 compile to under 128 VGPRs (W = 64:
+// 118 vs 114, no VGPR spills, ~160 SGPRs spilled to VGPR lanes either way), so 4 waves stay
+// resident per SIMD; the looser bound only changes the compiler's schedule, which measured
+// 1.3-1.4 ms per c4 step faster on two boxes (2: no better; W = 32 / 16 shares equal,
+// profiles/r04/ab_fused_waves.txt)
 #ifndef P2PG_FUSED_WAVES
-#define P2PG_FUSED_WAVES 4  // = 128 VGPRs: 4 waves per SIMD (the gathers spill a few registers per task, not per peer)
+#define P2PG_FUSED_WAVES 3
 #endif
 // MODE 0: the fused dense round above.
 // MODE 1, PO (push only): the first dense round after an update (16 < W <= 64, packed E) -- the
