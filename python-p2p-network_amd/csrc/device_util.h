@@ -298,10 +298,12 @@ int grid_tasks(int64_t ntasks) {
 // 32x -> 260 ms for the fused rounds).
 // The fused / grouped kernels keep their per-wave round totals in 32 bits.  A 32-peer task adds
 // at most 32 peers x 4096 messages x fanout 16 = 2^21 to any of them (relays; hubs, deg > HUB_T,
-// never go through these kernels, so wedges <= 32 x 64 words x 512 = 2^20), so no wave may take
-// more than 2^11 tasks: the grid is never smaller than that bound asks, whatever P2PG_FUSED_GRID,
-// the device size or V (config 4: ~2.4 tasks per wave).
-constexpr int64_t TASKS_PER_WAVE_MAX = 2048;
+// never go through these kernels, so wedges <= 32 x 64 words x 512 = 2^20), so a wave may take
+// at most 2^10 tasks (2^10 x 2^21 = 2^31 < 2^32, strictly): the grid is never smaller than that
+// bound asks, whatever P2PG_FUSED_GRID, the device size or V (config 4: ~2.4 tasks per wave).
+constexpr int64_t TASKS_PER_WAVE_MAX = 1024;
+static_assert(TASKS_PER_WAVE_MAX * (int64_t{32} * 4096 * 16) < (int64_t{1} << 32),
+              "per-wave 32-bit round totals could wrap");
 
 template <class F>
 int balanced_grid(F kernel, int64_t ntasks) {

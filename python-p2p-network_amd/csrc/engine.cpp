@@ -129,6 +129,8 @@ struct p2pg_engine {
   int32_t round = 0;
   bool done = false;
   bool have_state = false;
+  std::string failed;           // non-empty: the device state is inconsistent (a batched round's
+                                // push list overflowed); every step / run refuses until a reset
   // after a topology update: the graph the in-flight messages were sent on and its removed
   // slots, kept for the parents (record / deliveries) of the round that receives them
   int64_t* d_rowptr_arr = nullptr;
@@ -794,6 +796,7 @@ int p2pg_reset(p2pg_engine* e) {
   }
   e->round = 0;
   e->done = false;
+  e->failed.clear();
   e->begun = false;
   e->auto_round = -1;
   e->frontier_kept = true;
@@ -831,7 +834,12 @@ extern "C" {
 
 int p2pg_step_begin(p2pg_engine* e) {
   if (!e || !e->have_state) return fail(e, P2PG_ERR_STATE, "step_begin: no sources set");
+  if (!e->failed.empty()) return fail(e, P2PG_ERR_STATE, "step_begin: " + e->failed);
   if (e->begun) return fail(e, P2PG_ERR_STATE, "step_begin: the round has begun already");
+  // a rank-local graph marks its ghost slots REV_GHOST | id, which only the PART kernels (global
+  // ids set) know: the one-GPU kernels would index E with them
+  if ((e->cfg.flags & P2PG_FLAG_LOCAL_GRAPH) && !e->d_gid)
+    return fail(e, P2PG_ERR_STATE, "step_begin: a local-graph engine needs p2pg_set_global_ids first");
   if (e->done) return P2PG_OK;
   HIPCHK(e, hipSetDevice(e->cfg.device));
   DevState& s = e->st;
@@ -850,6 +858,7 @@ int p2pg_step_begin(p2pg_engine* e) {
 
 int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
   if (!e || !e->have_state) return fail(e, P2PG_ERR_STATE, "step: no sources set");
+  if (!e->failed.empty()) return fail(e, P2PG_ERR_STATE, "step: " + e->failed);
   if (e->done) {
     e->begun = false;
     if (out) {
@@ -981,8 +990,10 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
     bool use_e = false, have_tot = false;
     // the counters of this round are needed before its push only to choose the form (unless
     // that choice is clear already) and to size the sparse push's (peer, word) list (else
-    // bounded by the last round's pushed masks)
-    const bool blind = e->round > 0 && e->push_mode != 2 && clearly_sparse(e) && e->prev_sw > 0;
+    // bounded by the last round's pushed masks).  Not on a vertex-partitioned rank: rows other
+    // ranks pushed arrive by the exchange, so this rank's own pushed masks bound nothing
+    const bool blind = e->round > 0 && e->push_mode != 2 && !e->d_gid && clearly_sparse(e) &&
+                       e->prev_sw > 0;
     // (partitioned ranks: E for their local connections when part_dense, ghost rows travel)
     if (s.E[0] && (!e->d_gid || part_dense(e))) {
       if (e->push_mode == 2) {
@@ -1089,8 +1100,12 @@ int p2pg_step_end(p2pg_engine* e, p2pg_round_stats* out) { return p2pg_step(e, o
 // enqueued at once, each writing its counters to its own slot, and read with ONE host
 // synchronisation (c4: ~20 tail rounds of 0.05-0.2 ms kernels each paid a full host round trip).
 // Rounds enqueued after the run went quiet see an empty frontier and change nothing; they are
-// not reported and the engine stands where p2pg_step would have left it.  A (peer, word) list
-// that could not hold a round's frontier fails the call loudly (P2PG_ERR_STATE).
+// not reported and the engine stands where p2pg_step would have left it.  The list is sized by
+// a bound that holds for the batch's first round (its frontier words <= the masks pushed into it,
+// prev_sw) with room to spare for the others (decay: each round's frontier is ~2.5x smaller); a
+// later round whose frontier still outgrew it had its push truncated, so the call reports the
+// rounds before that one, fails (P2PG_ERR_STATE) and leaves the engine refusing every further
+// round until a reset (the device state past that round is not the run's).
 constexpr int BATCH_MAX = 8;
 
 static bool decay_batchable(const p2pg_engine* e) {
@@ -1112,9 +1127,9 @@ static int run_decay_batch(p2pg_engine* e, int32_t R, p2pg_round_stats* out, int
     HIPCHK(e, hipHostMalloc((void**)&e->h_bstats, sizeof(unsigned long long) * SLOT * BATCH_MAX));
   }
   HIPCHK(e, hipMemsetAsync(e->d_bstats, 0, sizeof(unsigned long long) * SLOT * R, e->stream));
-  // the list, sized once for the batch by the first round's bound
+  // the list, sized once for the batch: the first round's bound, doubled for the others
   SparseBufs b;
-  hipError_t lr = sparse_bufs(e, (int64_t)e->prev_sw, b);
+  hipError_t lr = sparse_bufs(e, 2 * (int64_t)e->prev_sw, b);
   if (lr != hipSuccess) return fail(e, P2PG_ERR_HIP, std::string("run (batch list): ") + hipGetErrorString(lr));
   const uint64_t words = (uint64_t)e->wlist_cap;  // no round of the batch grows the list
   unsigned long long* const stats0 = s.stats;
@@ -1142,10 +1157,14 @@ static int run_decay_batch(p2pg_engine* e, int32_t R, p2pg_round_stats* out, int
   *ran = 0;
   for (int32_t i = 0; i < R; ++i) {
     const unsigned long long* h = e->h_bstats + SLOT * i;
-    if ((int64_t)h[STAT_COUNT] > e->wlist_cap)
-      return fail(e, P2PG_ERR_STATE, "run: a batched round's frontier outgrew the sparse push list (" +
-                                         std::to_string(h[STAT_COUNT]) + " words listed, room for " +
-                                         std::to_string(e->wlist_cap) + ")");
+    if ((int64_t)h[STAT_COUNT] > e->wlist_cap) {
+      // round e->round's push was truncated: the rounds before it stand (reported), nothing after
+      e->failed = "round " + std::to_string(e->round) + " of a batched decay run outgrew its sparse push list (" +
+                  std::to_string(h[STAT_COUNT]) + " words listed, room for " + std::to_string(e->wlist_cap) +
+                  "); reset to run again";
+      e->done = true;
+      return fail(e, P2PG_ERR_STATE, "run: " + e->failed);
+    }
     uint64_t tot[STAT_N] = {0};
     for (int sh = 0; sh < STAT_SHARDS; ++sh)
       for (int q = 0; q < STAT_N; ++q) tot[q] += h[sh * STAT_N + q];
@@ -1195,9 +1214,13 @@ int p2pg_run(p2pg_engine* e, int32_t max_rounds, p2pg_round_stats* per_round,
       const int32_t R = std::min<int32_t>(br, max_rounds - n);
       p2pg_round_stats buf[BATCH_MAX];
       int32_t ran = 0;
-      if ((rc = run_decay_batch(e, R, buf, &ran)) < 0) return rc;
+      rc = run_decay_batch(e, R, buf, &ran);
       if (per_round) std::memcpy(per_round + n, buf, sizeof(p2pg_round_stats) * ran);
       n += ran;
+      if (rc < 0) {  // (the rounds that stand are reported)
+        if (n_rounds) *n_rounds = n;
+        return rc;
+      }
       rc = e->done ? 0 : 1;
       if (rc == 0) break;
       continue;

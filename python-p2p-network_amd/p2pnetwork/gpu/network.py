@@ -194,12 +194,13 @@ class GraphNetwork:
             while len(out) < max_rounds:
                 n = ctypes.c_int32()
                 chunk = min(max_rounds - len(out), len(buf))
-                rc = self._check(_lib.lib().p2pg_run(self._h, chunk, buf, ctypes.byref(n)))
-                for i in range(n.value):
+                rc = _lib.lib().p2pg_run(self._h, chunk, buf, ctypes.byref(n))
+                for i in range(n.value):  # rounds that stand are kept even if the call failed
                     st = RoundStats.from_c(buf[i])
                     out.append(st)
                     self.rounds.append(st)
                     self.message_count_send += st.relays
+                rc = self._check(rc)
                 if rc == 0 or n.value == 0:
                     break
             return out

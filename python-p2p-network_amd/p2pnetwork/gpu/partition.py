@@ -39,11 +39,7 @@ class VertexPartition:
         self.world, self.rank = world, rank
         V = graph.V
         rp = graph.rowptr
-        nnz = int(rp[-1])
-        # bounds[q] = first peer of rank q (edge-balanced), bounds[world] = V
-        targets = (np.arange(1, world, dtype=np.float64) * nnz / world)
-        cuts = np.searchsorted(rp[:-1], targets, side="left")
-        self.bounds = np.concatenate([[0], np.maximum.accumulate(cuts), [V]]).astype(np.int64)
+        self.bounds = self.ranges(graph, world)
         lo, hi = int(self.bounds[rank]), int(self.bounds[rank + 1])
         self.lo, self.hi = lo, hi
         nb = graph.colidx[rp[lo]:rp[hi]].astype(np.int64)
@@ -54,18 +50,22 @@ class VertexPartition:
         self.gid = np.concatenate([gid, [V]]).astype(np.int32)
         self.V_local = len(self.gid)
         self.dummy = self.V_local - 1
-        owned_local = np.searchsorted(self.gid, np.arange(lo, hi))
-        self.owned_local = owned_local.astype(np.int64)
+        # global -> local id of every held peer by one dense map (a binary search per slot took
+        # ~2 minutes per rank at config 5's 100M peers; the map is 4 B per global peer)
+        loc = np.empty(V, dtype=np.int32)
+        loc[gid] = np.arange(len(gid), dtype=np.int32)
+        owned_local = loc[lo:hi].astype(np.int64)
+        self.owned_local = owned_local
         # local CSR: owned rows mapped (monotone map keeps rows ascending), ghost rows empty
         deg_local = np.zeros(self.V_local, dtype=np.int64)
         deg_local[owned_local] = np.diff(rp[lo:hi + 1])
         self.rowptr = np.concatenate([[0], np.cumsum(deg_local)]).astype(np.int64)
-        self.colidx = np.searchsorted(self.gid, nb).astype(np.int32)
+        self.colidx = loc[nb]
         # exchange lists, peer by peer, each sorted by global id
         owner = self.owner(ghosts)
         self.recv_counts = np.bincount(owner, minlength=world).astype(np.int64)
         self.recv_counts[rank] = 0
-        self.recv_local = np.searchsorted(self.gid, ghosts).astype(np.int32)  # ghosts by owner
+        self.recv_local = loc[ghosts]  # ghosts by owner
         rows = np.repeat(np.arange(lo, hi, dtype=np.int64), np.diff(rp[lo:hi + 1]))
         is_remote = (nb < lo) | (nb >= hi)
         pairs_peer = self.owner(nb[is_remote])
@@ -79,7 +79,17 @@ class VertexPartition:
             send.append(s)
         send = np.concatenate(send) if send else np.zeros(0, dtype=np.int64)
         self.send_counts = counts
-        self.send_local = np.searchsorted(self.gid, send).astype(np.int32)
+        self.send_local = loc[send]
+
+    @staticmethod
+    def ranges(graph, world):
+        """bounds[q] = first peer of rank q (contiguous ranges balanced by connection count),
+        bounds[world] = V."""
+        rp = graph.rowptr
+        nnz = int(rp[-1])
+        targets = (np.arange(1, world, dtype=np.float64) * nnz / world)
+        cuts = np.searchsorted(rp[:-1], targets, side="left")
+        return np.concatenate([[0], np.maximum.accumulate(cuts), [graph.V]]).astype(np.int64)
 
     def ghost_senders(self, graph):
         """(ghost_deg [V_local], slot_pos [local slots]) for p2pg_set_ghost_senders: a ghost's

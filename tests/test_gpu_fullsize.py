@@ -13,12 +13,14 @@
   the C oracle, in every push form.
 Each test prints nothing for up to ~2 minutes (graph generation and the CPU oracle)."""
 import os
+from types import SimpleNamespace
 
 import numpy as np
 import pytest
 
 from oracle import coracle
 from test_gpu_parity import assert_rounds_equal
+from test_gpu_partition import _assert_same_rounds
 
 pytestmark = pytest.mark.gpu
 
@@ -38,30 +40,121 @@ def c5_net(g, thr, **kw):
     return GraphNetwork(g, mode="flood", churn_threshold_value=thr, churn_seed=CSEED, **kw)
 
 
-def test_config5_full_size_flood_churn(config5):
+# Config 5's own form is the 1-D vertex partition (BASELINE.json configs[4]).  Two ranks are what
+# one MI355X holds at the full 100M peers: each owns 50M peers and keeps 16.7M ghosts, i.e. 66.7M
+# rows x 512 B x 3 planes + 2 x 16.7M x 65 int64 of record buffers = 122 GB per rank.
+C5_WORLD = 2
+
+
+def _digest(a):
+    import xxhash
+    return xxhash.xxh3_128_digest(np.ascontiguousarray(a))
+
+
+@pytest.fixture(scope="module")
+def config5_run(config5):
+    """Config 5's 4096-flood run on one engine (then reset and run again): per-round counters,
+    |seen set| per peer, words 0 and 63, and a 128-bit digest of every word column over each
+    rank's owned range of the C5_WORLD-rank vertex partition (the partitioned run is held to
+    those).  The whole plane never comes to the host (51 GB): one word column at a time."""
+    from p2pnetwork.gpu.partition import VertexPartition
     g, src, thr = config5
-    M = len(src)
-    deg = g.degree()
+    bounds = VertexPartition.ranges(g, C5_WORLD)
     with c5_net(g, thr) as net:
         net.broadcast(src)
         a = net.run()
         pop = np.zeros(g.V, dtype=np.int64)  # |seen set| per peer, 64 words at a time
-        cols = {}
-        for w in range(M // 64):
+        cols, dig = {}, {}
+        for w in range(len(src) // 64):
             col = net.seen_word(w)
             pop += np.bitwise_count(col)
+            for q in range(C5_WORLD):
+                dig[w, q] = _digest(col[bounds[q]:bounds[q + 1]])
             if w in (0, 63):
                 cols[w] = col
             del col
         net.reset()
         b = net.run()
+    return dict(rounds=a, rounds_again=b, pop=pop, cols=cols, dig=dig, bounds=bounds)
+
+
+def _c5_partitioned(g, src, thr, per_rank, record=False):
+    """Config 5 as a C5_WORLD-rank vertex partition: real engines as threads on the one GPU,
+    records moved between them by device copies (ThreadTransport), the engine streams waiting
+    for the copies (PartitionedNetwork._ready), the next round's interior peers overlapping the
+    exchange.  per_rank(rank, net, rounds) runs in the rank's thread before its engine closes."""
+    import threading
+    from p2pnetwork.gpu import PartitionedNetwork
+    from test_gpu_partition import ThreadTransport
+    shared = {"slots": [None] * C5_WORLD, "barrier": threading.Barrier(C5_WORLD)}
+    out, errors = [None] * C5_WORLD, []
+
+    def rank_main(rank):
+        try:
+            net = PartitionedNetwork(g, C5_WORLD, rank, ThreadTransport(shared, rank), mode="flood",
+                                     churn_threshold_value=thr, churn_seed=CSEED, record=record)
+            with net.net:
+                net.broadcast(src)
+                rounds = net.run()
+                out[rank] = per_rank(rank, net, rounds)
+        except BaseException as exc:  # surface in the main thread; unblock the other rank
+            errors.append(exc)
+            shared["barrier"].abort()
+
+    th = [threading.Thread(target=rank_main, args=(r,)) for r in range(C5_WORLD)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=800)
+    if errors:
+        raise errors[0]
+    return out
+
+
+@pytest.mark.timeout(900)
+def test_config5_vertex_partitioned_full_size(config5, config5_run):
+    """Config 5 in its own form: 100M-peer WS k=8 beta=0.1, churn 0.05, 4096 floods, vertex-
+    partitioned over 2 ranks (50M owned + 16.7M ghost rows each; records of 1 + 64 int64 per live
+    boundary row, list segments, >= 2^30-word record buffers) -- every owned word column of every
+    rank == the one-engine run's (digest per word and rank range), every global per-round counter
+    == the one-engine run's.  Anchors: the relay node.py:106-120 with the lost sends of
+    nodeconnection.py:123-126; the cross-host fan-out it replaces, nodeconnection.py:107-160."""
+    g, src, thr = config5
+    ref = config5_run
+    M = len(src)
+
+    def check(rank, net, rounds):
+        p = net.part
+        assert p.lo == ref["bounds"][rank] and p.hi == ref["bounds"][rank + 1]
+        assert p.V_local > 60_000_000 and len(p.send_local) * (1 + M // 64) > 1 << 30
+        bad = []
+        own = p.owned_local
+        buf = np.empty(len(own), dtype=np.uint64)
+        for w in range(M // 64):
+            np.take(net.net.seen_word(w), own, out=buf)
+            if _digest(buf) != ref["dig"][w, rank]:
+                bad.append(w)
+            if w == 0 and rank == 0:  # one column exactly, not only by digest
+                np.testing.assert_array_equal(buf, ref["cols"][0][p.lo:p.hi])
+        return rounds, bad, [r.push_form for r in net.local_rounds]
+
+    res = _c5_partitioned(g, src, thr, check)
+    for rank, (rounds, bad, _) in enumerate(res):
+        assert not bad, f"rank {rank}: owned seen words {bad} differ from the one-engine run"
+        _assert_same_rounds(rounds, ref["rounds"])  # global counters, every round
+
+
+def test_config5_full_size_flood_churn(config5, config5_run):
+    g, src, thr = config5
+    M = len(src)
+    deg = g.degree()
+    a, b, pop, cols = (config5_run[k] for k in ("rounds", "rounds_again", "pop", "cols"))
     assert [r.as_dict() for r in a] == [r.as_dict() for r in b]
     delivered = int(pop.sum())
     assert delivered == sum(r.new_deliveries for r in a)
     assert 0.99 * g.V * M < delivered <= g.V * M  # churn loses sends, not (on WS) whole peers
     # every first receipt relays deg - 1 (the sender excluded), the origin deg: node.py:106-116
     assert sum(r.relays for r in a) == int((pop * (deg - 1)).sum()) + M
-    del pop
     for w, col in cols.items():
         with c5_net(g, thr, msg_id_base=64 * w) as sub:
             sub.broadcast(src[64 * w:64 * w + 64])
@@ -104,7 +197,9 @@ def test_config5_full_size_words_match_c_oracle(config5):
 
 def test_config5_word0_hop_parent_match_c_oracle(config5):
     """Messages 0..63 of config 5: first-receipt round and lowest-id surviving sender of all
-    100M peers, bit for bit against the C oracle (which re-draws every churn decision)."""
+    100M peers, bit for bit against the C oracle (which re-draws every churn decision) -- on one
+    engine, and as the 2-rank vertex partition (every owned row of each rank; parents across the
+    rank boundary are ghost senders whose frontier rows arrived as records)."""
     g, src, thr = config5
     with c5_net(g, thr, record=True) as net:
         net.broadcast(src[:64])
@@ -114,8 +209,23 @@ def test_config5_word0_hop_parent_match_c_oracle(config5):
                       record=True)
     assert_rounds_equal(rounds, ora.rounds)
     assert np.array_equal(hop, ora.hop)
-    del hop, ora.hop
+    del hop
     assert np.array_equal(parent, ora.parent)
+    del parent
+
+    def check(rank, pnet, prounds):
+        p = pnet.part
+        h, par = pnet.net.hop_parent()
+        own = p.owned_local
+        step = 1 << 22
+        for a in range(0, len(own), step):  # owned rows in global order, 4M at a time
+            rows = own[a:a + step]
+            assert np.array_equal(h[rows], ora.hop[p.lo + a:p.lo + a + len(rows)]), f"rank {rank} hop"
+            assert np.array_equal(par[rows], ora.parent[p.lo + a:p.lo + a + len(rows)]), f"rank {rank} parent"
+        return prounds
+
+    for prounds in _c5_partitioned(g, src[:64], thr, check, record=True):
+        _assert_same_rounds(prounds, [SimpleNamespace(**r) for r in ora.rounds])
 
 
 @pytest.mark.parametrize("push", ["auto", "atomic", "store_unfused"])

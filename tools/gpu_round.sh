@@ -3,7 +3,7 @@
 # rocprofv3 kernel stats of the c4 bench command.
 #   bash tools/gpu_round.sh <tag>
 set -o pipefail
-tag=${1:-r03}
+tag=${1:?usage: bash tools/gpu_round.sh <tag>}
 mkdir -p gpurun_out/$tag
 export TMPDIR=/tmp
 if [ -z "$SKIP_SUITE" ]; then
@@ -18,3 +18,5 @@ for m in 2048 1024 512; do
 done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$tag/stats -o c4 -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/$tag/prof_bench.json 2> gpurun_out/$tag/prof.err || { tail -20 gpurun_out/$tag/prof.err; exit 1; }
 echo prof ok
+timeout -k 10 200 python3 tools/round_profile.py c4 1 > gpurun_out/$tag/rounds_c4.json || exit 1
+echo rounds ok
