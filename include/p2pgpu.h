@@ -156,6 +156,11 @@ int p2pg_read_seen_word(p2pg_engine* e, int32_t w, uint64_t* out);
  * (a dense round after a dense round).                                                  */
 #define P2PG_KCLASS_N 8
 int p2pg_kernel_times(p2pg_engine* e, double ms[P2PG_KCLASS_N], int64_t launches[P2PG_KCLASS_N]);
+/* With P2PG_FLAG_TIMING: only launches of the classes in mask (bit i = class i; default all)
+ * are bracketed by HIP events -- two event records per launch cost ~2.7 us of stream time each
+ * (0.8 ms per config-4 broadcast), so a measurement can time its dominant kernel alone.
+ * (Instrumentation; the reference has none -- its only counters are node.py:65-67.)       */
+int p2pg_set_timed_classes(p2pg_engine* e, uint32_t mask);
 /* ---- vertex-partitioned runs (one engine per GPU) ---------------------
  * The caller loads the rank's LOCAL graph: owned peers plus ghost peers (remote neighbours),
  * all numbered in ascending GLOBAL id order (so lowest-id tie-breaks are unchanged); ghosts

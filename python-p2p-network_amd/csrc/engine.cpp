@@ -99,6 +99,8 @@ struct p2pg_engine {
   bool sparse_lp = true;       // sparse rounds: lane-parallel scatter (relay_sparse.hip) when
                                // the rows allow it; P2PG_SPARSE_LP=0 keeps the per-source one
   bool skip_frontier = false;  // p2pg_run, not its last two allowed rounds: fused rounds may skip F
+  bool partial_f = true;       // ... and updates / the last dense pull write its nonzero words
+                               // only (P2PG_PARTIAL_F=0: whole rows, A/B)
   bool frontier_kept = true;   // F[(round-1)&1] holds the last round's first receipts
   bool frontier_kept_prev = true;  // ... and F[round&1] the round before (delivery parents)
   uint64_t prev_aw = 0, prev_av = 0;  // active words / rows of the previous round
@@ -117,6 +119,12 @@ struct p2pg_engine {
   DevState st{};
   size_t plane_bytes = 0, bm_bytes = 0;
   unsigned long long* h_stats = nullptr;  // pinned
+  // The round counters accumulate on the device across rounds (no per-round clearing launch): a
+  // round's counters are the difference to stats_base, the copy read at the end of the round
+  // before.  stats_clear: the device counters must be zeroed first (new state, reset, restore, or
+  // an out-of-round launch that counted: a topology update's re-push, a snapshot's materialize)
+  unsigned long long stats_base[STAT_N * STAT_SHARDS] = {0};
+  bool stats_clear = true;
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
   hipEvent_t ev[2] = {nullptr, nullptr};
@@ -124,6 +132,7 @@ struct p2pg_engine {
   // sync (no extra host synchronisation inside a round)
   std::vector<hipEvent_t> ev_pool;
   std::vector<int> ev_cls;  // class of pending pair i (events 2i, 2i+1)
+  uint32_t timed_mask = (1u << P2PG_KCLASS_N) - 1u;  // classes whose launches get events
   double kms[P2PG_KCLASS_N] = {0};
   int64_t klaunch[P2PG_KCLASS_N] = {0};
   int32_t round = 0;
@@ -312,7 +321,7 @@ DevGraph graph_for_arrivals(const p2pg_engine* e, int32_t r) {
 // Timed launch: kernel class cls in [0, P2PG_KCLASS_N) (see include/p2pgpu.h).
 template <class F>
 int timed(p2pg_engine* e, int cls, F&& launch) {
-  const bool timing = (e->cfg.flags & P2PG_FLAG_TIMING) != 0;
+  const bool timing = (e->cfg.flags & P2PG_FLAG_TIMING) != 0 && ((e->timed_mask >> cls) & 1u);
   size_t slot = 0;
   if (timing) {
     slot = e->ev_cls.size();
@@ -440,6 +449,16 @@ bool still_dense(const p2pg_engine* e) {
   return av > 0.0 && aw >= e->e_thresh * av * (double)e->W && av >= e->v_thresh * (double)e->v_conn;
 }
 
+// Inside p2pg_run (not its last two allowed rounds, no hop/parent records): may this round's update
+// / last dense pull write only the nonzero words of its frontier rows (RoundParams::store_f == 2)?
+// Packed rows only (16 < W <= 64: AW planes, one peer per wave), not on a partitioned rank.  A
+// whole 512 B row write per active peer was ~40 % of the sparse update's bytes; the words are
+// read back only through the AW mask (sparse push list, push-only pass, per-source scatter).
+bool partial_frontier(const p2pg_engine* e, bool skip) {
+  return skip && !e->st.hop && e->st.AW[0] && e->W > GROUPED_W_MAX && e->W <= 64 && !e->d_gid &&
+         e->partial_f;
+}
+
 // Can this vertex-partitioned rank (global ids set) take the dense rounds (E pushes, fused and
 // pull-only passes in their PART form, relay_kernels.hip)?  Packed rows over 16 < W <= 64 and
 // two E planes; otherwise its gossip pushes go by row atomics only.
@@ -552,6 +571,7 @@ int alloc_state(p2pg_engine* e) {
 #endif
   if ((rc = A((void**)&e->d_src, sizeof(int32_t) * (e->M ? e->M : 1)))) return rc;
   e->have_state = true;
+  e->stats_clear = true;
   return P2PG_OK;
 }
 
@@ -583,6 +603,7 @@ int p2pg_create(const p2pg_config* cfg, p2pg_engine** out) {
   if (const char* f = std::getenv("P2PG_UPDATE_PUSH")) e->update_push = std::atoi(f);
   if (const char* f = std::getenv("P2PG_RUN_BATCH")) e->batch_rounds = std::atoi(f);
   if (const char* f = std::getenv("P2PG_DECAY_PRED")) e->decay_pred = std::strcmp(f, "0") != 0;
+  if (const char* f = std::getenv("P2PG_PARTIAL_F")) e->partial_f = std::strcmp(f, "0") != 0;
   if (const char* m = std::getenv("P2PG_GOSSIP_PUSH"))
     e->push_mode = !std::strcmp(m, "atomic") ? 1 : (!std::strcmp(m, "store") ? 2 : 0);
   HIPCHK(e, hipSetDevice(cfg->device));
@@ -797,6 +818,7 @@ int p2pg_reset(p2pg_engine* e) {
   e->round = 0;
   e->done = false;
   e->failed.clear();
+  e->stats_clear = true;
   e->begun = false;
   e->auto_round = -1;
   e->frontier_kept = true;
@@ -843,7 +865,11 @@ int p2pg_step_begin(p2pg_engine* e) {
   if (e->done) return P2PG_OK;
   HIPCHK(e, hipSetDevice(e->cfg.device));
   DevState& s = e->st;
-  HIPCHK(e, hipMemsetAsync(s.stats, 0, STAT_BYTES, e->stream));
+  if (e->stats_clear) {
+    HIPCHK(e, hipMemsetAsync(s.stats, 0, STAT_BYTES, e->stream));
+    std::memset(e->stats_base, 0, sizeof(e->stats_base));
+    e->stats_clear = false;
+  }
   e->begun = true;
   if (!split_round(e)) return P2PG_OK;
   // phase 0: peers without a ghost neighbour, which need none of the rows still in transit
@@ -881,6 +907,8 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
   e->begun = false;
   const bool gossip = e->cfg.mode == P2PG_MODE_GOSSIP;
   bool fused_round = false, up_round = false;
+  // the update / pull-only pass of this round (fused and update+push rounds set their own)
+  if (gossip && partial_frontier(e, e->skip_frontier)) p.store_f = 2;
   uint64_t host_new = 0, host_relays = 0, host_av = 0, host_aw = 0, host_wedge = 0, host_degact = 0;
   if (e->round == 0) {
     if ((rc = timed(e, 0, [&] { return launch_zero_rows(s.F[0], e->W, e->d_src, e->M, e->stream); }))) return rc;
@@ -971,7 +999,8 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
     if (r2) return r2;
     for (int i = 0; i < STAT_N; ++i) tot[i] = 0;
     for (int sh = 0; sh < STAT_SHARDS; ++sh)
-      for (int i = 0; i < STAT_N; ++i) tot[i] += e->h_stats[sh * STAT_N + i];
+      for (int i = 0; i < STAT_N; ++i)
+        tot[i] += e->h_stats[sh * STAT_N + i] - e->stats_base[sh * STAT_N + i];
     if (e->round == 0) {
       tot[ST_NEW] = host_new;
       tot[ST_RELAYS] = host_relays;
@@ -1045,6 +1074,7 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
     e->auto_round = e->round;
   }
   if ((rc = read_stats())) return rc;
+  std::memcpy(e->stats_base, e->h_stats, sizeof(e->stats_base));  // the next round counts from here
   if ((rc = check_scatter_list(e, e->h_stats[STAT_COUNT]))) return rc;
   if (e->auto_round == e->round)  // the round's own pack landed with its counters
     for (int q = 0; q + 1 < (int)e->send_seg.size(); ++q) e->auto_cnt[q] = (int64_t)e->h_seg_cnt[q];
@@ -1061,7 +1091,7 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
 #endif
   const bool active = tot[ST_NEW] != 0;
   e->frontier_kept_prev = e->frontier_kept;
-  e->frontier_kept = !((fused_round || up_round) && !p.store_f && active);
+  e->frontier_kept = !(((fused_round || up_round) && !p.store_f) || p.store_f == 2) || !active;
   if (out) {
     out->round = e->round;
     out->active = active ? 1 : 0;
@@ -1118,7 +1148,9 @@ static bool decay_batchable(const p2pg_engine* e) {
          e->last_new * 16 < (uint64_t)e->V;  // the tail: small rounds, where the syncs dominate
 }
 
-static int run_decay_batch(p2pg_engine* e, int32_t R, p2pg_round_stats* out, int32_t* ran) {
+// n_left: rounds the p2pg_run call may still run (its last two keep their frontier rows whole).
+static int run_decay_batch(p2pg_engine* e, int32_t R, p2pg_round_stats* out, int32_t* ran,
+                           int32_t n_left) {
   constexpr size_t SLOT = STAT_COUNT + 1;  // counters + the sparse list's fill count
   DevState& s = e->st;
   HIPCHK(e, hipSetDevice(e->cfg.device));
@@ -1135,10 +1167,13 @@ static int run_decay_batch(p2pg_engine* e, int32_t R, p2pg_round_stats* out, int
   unsigned long long* const stats0 = s.stats;
   const DevGraph g = graph(e);
   int rc = P2PG_OK;
+  bool partial[BATCH_MAX] = {false};
   for (int32_t i = 0; i < R && rc == P2PG_OK; ++i) {
     s.stats = e->d_bstats + SLOT * i;
     RoundParams p = params(e);
     p.round = e->round + i;
+    if (partial_frontier(e, i + 2 < n_left)) p.store_f = 2;
+    partial[i] = p.store_f == 2;
     rc = timed(e, 4, [&] { return launch_gossip_update(g, s, p, e->stream); });
     if (rc == P2PG_OK && s.hop) rc = timed(e, 3, [&] { return launch_record(g, s, p, e->stream); });
     p.dedup_push = e->push_dedup != 0;  // decay phase
@@ -1184,7 +1219,7 @@ static int run_decay_batch(p2pg_engine* e, int32_t R, p2pg_round_stats* out, int
     o.reserved_ = 0;
     e->total_relays += tot[ST_RELAYS];
     e->frontier_kept_prev = e->frontier_kept;
-    e->frontier_kept = true;
+    e->frontier_kept = !(partial[i] && active);
     e->prev2_aw = e->prev_aw;
     e->prev2_av = e->prev_av;
     e->prev2_new = e->last_new;
@@ -1214,7 +1249,7 @@ int p2pg_run(p2pg_engine* e, int32_t max_rounds, p2pg_round_stats* per_round,
       const int32_t R = std::min<int32_t>(br, max_rounds - n);
       p2pg_round_stats buf[BATCH_MAX];
       int32_t ran = 0;
-      rc = run_decay_batch(e, R, buf, &ran);
+      rc = run_decay_batch(e, R, buf, &ran, max_rounds - n);
       if (per_round) std::memcpy(per_round + n, buf, sizeof(p2pg_round_stats) * ran);
       n += ran;
       if (rc < 0) {  // (the rounds that stand are reported)
@@ -1656,6 +1691,7 @@ int p2pg_update_edges(p2pg_engine* e, int64_t n_add, const int32_t* add, int64_t
     }
     e->consume_next = true;
     e->last_push_e = false;
+    e->stats_clear = true;  // the re-push above counted into the round counters
     // keep the old rows for the parents of the receiving round (record / deliveries)
     e->d_rowptr_arr = e->d_rowptr;
     e->d_colidx_arr = e->d_colidx;
@@ -1768,6 +1804,7 @@ int p2pg_snapshot(p2pg_engine* e, void* buf, int64_t cap) {
     hipError_t lr = launch_materialize(graph(e), s, p, false, e->stream);
     if (lr != hipSuccess) return fail(e, P2PG_ERR_HIP, std::string("snapshot: ") + hipGetErrorString(lr));
     e->last_push_e = false;
+    e->stats_clear = true;
   }
   HIPCHK(e, hipStreamSynchronize(e->stream));
   const int64_t need = snapshot_bytes(e);
@@ -1878,6 +1915,13 @@ int p2pg_kernel_times(p2pg_engine* e, double ms[P2PG_KCLASS_N], int64_t launches
     if (ms) ms[i] = e->kms[i];
     if (launches) launches[i] = e->klaunch[i];
   }
+  return P2PG_OK;
+}
+
+int p2pg_set_timed_classes(p2pg_engine* e, uint32_t mask) {
+  if (!e) return P2PG_ERR_ARG;
+  if (mask >> P2PG_KCLASS_N) return fail(e, P2PG_ERR_ARG, "set_timed_classes: unknown class bit");
+  e->timed_mask = mask;
   return P2PG_OK;
 }
 

@@ -197,6 +197,12 @@ struct PullStage {
 
 // One target's prefetch stage for k_gossip_fused: as PullStage, with 32-bit peer and slot ids
 // (gossip slot ids are uint32: rev[]) -- the fused kernel's scalar registers are the scarce ones.
+// Is word w of v's frontier row live?  Packed rows (AW planes, W <= 64): iff bit w of its AW mask
+// (rows written with RoundParams::store_f == 2 hold stale words elsewhere); else every word.
+__device__ __forceinline__ bool aw_has(const uint64_t* __restrict__ AW, int64_t v, int w) {
+  return !AW || ((ldc(AW + v) >> w) & 1ull);
+}
+
 struct FusedStage {
   int32_t u;        // the target peer (-1: none)
   uint32_t beg, end;
@@ -739,16 +745,24 @@ __global__ __launch_bounds__(256) void k_gossip_update(DevGraph g, DevState st,
 // k_gossip_update (every gossip test runs it).
 struct UpdStage {
   int64_t u;   // touched peer (-1: none)
-  int64_t u2;  // PAIR: a second touched peer of the same task (-1: none)
+  int64_t u2;  // PAIR / DUAL: a second touched peer of the same task (-1: none)
   uint64_t x;  // this lane's push word
   uint64_t s;  // this lane's seen word (where x != 0)
+  uint64_t x2; // DUAL: the second peer's push word and seen word
+  uint64_t s2;
 };
 
-// PAIR (W <= 32): two touched peers of a task per stage, lanes 0-31 the first, 32-63 the second
-// (one peer per wave leaves half the wave idle at these widths and pays the per-peer wave work
-// once per peer).
-template <bool PAIR = false>
+// NP = 1: one touched peer per stage, lane = word.
+// NP = 2, PAIR (W <= 32): two touched peers of a task per stage, lanes 0-31 the first, 32-63 the
+//   second (one peer per wave leaves half the wave idle at these widths and pays the per-peer wave
+//   work once per peer).
+// NP = 3, DUAL (W <= 64): two touched peers of a task per stage, lane = word of both (two words
+//   per lane).  The update is latency-bound: every stage waits for one memory round trip (its
+//   rows' loads) and a wave consumed ONE peer per trip (c4 round 9: ~1.3 us per peer per wave at
+//   ~3.5 TB/s); two rows per trip halve the trips.
+template <int NP = 1>
 __global__ __launch_bounds__(256) void k_gossip_update1(DevGraph g, DevState st, RoundParams p) {
+  constexpr bool PAIR = NP == 2, DUAL = NP == 3;
   const int lane = threadIdx.x & 63;
   const int wib = wave_in_block();
   const int64_t V = g.V;
@@ -790,15 +804,19 @@ __global__ __launch_bounds__(256) void k_gossip_update1(DevGraph g, DevState st,
   };
   auto issue_x = [&](UpdStage& q) {
     q.u = next_peer();
-    q.u2 = (PAIR && q.u >= 0 && it_rest) ? next_peer() : -1;  // never across a task boundary
+    q.u2 = ((PAIR || DUAL) && q.u >= 0 && it_rest) ? next_peer() : -1;  // never across a task boundary
     q.x = 0;
     q.s = 0;
+    q.x2 = 0;
+    q.s2 = 0;
     const int64_t me = hl ? q.u2 : q.u;
     if (me >= 0 && valid) q.x = nx[me * W + wl];
+    if (DUAL && q.u2 >= 0 && valid) q.x2 = nx[q.u2 * W + wl];
   };
   auto issue_s = [&](UpdStage& q) {
     const int64_t me = hl ? q.u2 : q.u;
     if (me >= 0 && q.x) q.s = st.seen[me * W + wl];
+    if (DUAL && q.u2 >= 0 && q.x2) q.s2 = st.seen[q.u2 * W + wl];
   };
 
   int64_t ct = -1;  // task of the consumed peers
@@ -807,31 +825,22 @@ __global__ __launch_bounds__(256) void k_gossip_update1(DevGraph g, DevState st,
     if (ct >= 0 && lane == 0) put_active(st.A[cur], ct, aw, p);
     aw = 0;
   };
-  auto consume = [&](const UpdStage& q) {
-    if ((q.u >> 5) != ct) {
-      finish_task();
-      ct = q.u >> 5;
-    }
-    const int64_t u = hl ? q.u2 : q.u;  // this lane's peer (PAIR: the stage's second one above 32)
-    const int64_t deg1 = ldc(g.rowptr + q.u + 1) - ldc(g.rowptr + q.u);
-    const int64_t deg2 = PAIR && q.u2 >= 0 ? ldc(g.rowptr + q.u2 + 1) - ldc(g.rowptr + q.u2) : 0;
-    const int64_t deg = hl ? deg2 : deg1;
+  // one peer u (lanes: its words x / seen s) of this lane's stage
+  // (wm_all: the stage's ballot of new words; PAIR: this lane's half of it is its peer's)
+  auto consume_one = [&](int64_t u, int64_t deg, uint64_t x, uint64_t s, uint64_t wm_all, int shift) {
     // relays per first receipt: gossip min(k, deg); flood (rows materialized by a topology
     // update) deg - 1, the sender's connection being excluded (node.py:106-112)
     const uint64_t fan = p.mode == 0 ? (uint64_t)(deg > 0 ? deg - 1 : 0)
                                      : (uint64_t)(deg < p.fanout ? deg : p.fanout);
-    const uint64_t x = q.x, s = q.s;
     if (x) {
       st_prow(&nx[u * W + wl], 0ull);
       c[ST_AUX] += 1;  // touched (pushed-to) words consumed
     }
     const uint64_t nw = x & ~s;
-    const uint64_t wmb = __ballot(nw != 0ull);
-    const uint64_t wm1 = PAIR ? (wmb & 0xFFFFFFFFull) : wmb, wm2 = PAIR ? (wmb >> 32) : 0ull;
-    const uint64_t wm = hl ? wm2 : wm1;  // this lane's peer's new words
+    const uint64_t wm = PAIR ? (wm_all >> shift) & 0xFFFFFFFFull : wm_all;
     if (wm && st.AW[cur] && wl == 0) st.AW[cur][u] = wm;
     if (nw) st_prow(&st.seen[u * W + wl], s | nw);
-    if (valid && wm) st_prow(&Fc[u * W + wl], nw);
+    if (valid && wm && (p.store_f != 2 || nw)) st_prow(&Fc[u * W + wl], nw);  // (2: AW-valid rows)
     if (nw) {
       const uint64_t pc = (uint64_t)__popcll(nw);
       c[ST_NEW] += pc;
@@ -839,11 +848,34 @@ __global__ __launch_bounds__(256) void k_gossip_update1(DevGraph g, DevState st,
       c[ST_ACTIVE_W] += 1;
       c[ST_WEDGES] += (uint64_t)deg;
     }
-    if (wm1) aw |= 1u << (q.u & 31);
-    if (wm2) aw |= 1u << (q.u2 & 31);
     if (wm && wl == 0) {
       c[ST_ACTIVE_V] += 1;
       c[ST_DEG_ACT] += (uint64_t)deg;
+    }
+  };
+  auto consume = [&](const UpdStage& q) {
+    if ((q.u >> 5) != ct) {
+      finish_task();
+      ct = q.u >> 5;
+    }
+    const int64_t deg1 = ldc(g.rowptr + q.u + 1) - ldc(g.rowptr + q.u);
+    const int64_t deg2 = (PAIR || DUAL) && q.u2 >= 0 ? ldc(g.rowptr + q.u2 + 1) - ldc(g.rowptr + q.u2) : 0;
+    const uint64_t nw1 = q.x & ~q.s;
+    const uint64_t wmb = __ballot(nw1 != 0ull);
+    if (PAIR) {
+      // lanes 0-31 serve q.u, lanes 32-63 q.u2
+      const uint64_t wm1 = wmb & 0xFFFFFFFFull, wm2 = wmb >> 32;
+      consume_one(hl ? q.u2 : q.u, hl ? deg2 : deg1, q.x, q.s, wmb, hl ? 32 : 0);
+      if (wm1) aw |= 1u << (q.u & 31);
+      if (wm2) aw |= 1u << (q.u2 & 31);
+      return;
+    }
+    consume_one(q.u, deg1, q.x, q.s, wmb, 0);
+    if (wmb) aw |= 1u << (q.u & 31);
+    if (DUAL && q.u2 >= 0) {
+      const uint64_t wmb2 = __ballot((q.x2 & ~q.s2) != 0ull);
+      consume_one(q.u2, deg2, q.x2, q.s2, wmb2, 0);
+      if (wmb2) aw |= 1u << (q.u2 & 31);
     }
   };
   // three stages rotate by unrolling (a register copy of a load in flight would wait for it)
@@ -1469,6 +1501,9 @@ __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st,
   const int W = st.W;
   const int cur = p.round & 1;
   const uint64_t* __restrict__ Fc = st.F[cur];
+  // packed rows: a frontier word counts only under the row's AW mask (an update that ran with
+  // RoundParams::store_f == 2 leaves stale words outside it)
+  const uint64_t* __restrict__ AWc = W <= 64 ? st.AW[cur] : nullptr;
   const int64_t nwords = (V + 31) >> 5;
   const int64_t ntasks = nwords + ((n_hub + 63) >> 6);
   const int nslices = (W + 63) >> 6;
@@ -1504,7 +1539,7 @@ __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st,
       uint64_t f1 = 0;
       uint32_t rv1 = 0;
       if (b1 >= 0) {
-        if (lane < W) f1 = Fc[(base + b1) * W + lane];
+        if (lane < W && aw_has(AWc, base + b1, lane)) f1 = Fc[(base + b1) * W + lane];
         rv1 = load_nbr(rb1, (int)deg1);
       }
       while (b1 >= 0) {
@@ -1512,7 +1547,7 @@ __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st,
         uint64_t f2 = 0;
         uint32_t rv2 = 0;
         if (b2 >= 0) {
-          if (lane < W) f2 = Fc[(base + b2) * W + lane];
+          if (lane < W && aw_has(AWc, base + b2, lane)) f2 = Fc[(base + b2) * W + lane];
           rv2 = load_nbr(rb2, (int)deg2);
         }
         scatter_row<CHURN, K, STORE_E, 0, PART>(g, st, p, L, lane, base + b1, rb1, deg1, 0, 0, f1, rv1, 0,
@@ -1551,7 +1586,7 @@ __global__ __launch_bounds__(256) void k_gossip_scatter(DevGraph g, DevState st,
       const uint32_t rv = load_nbr(rb + nb, nn);
       for (int sl = 0; sl < nslices; ++sl) {
         const int w = sl * 64 + lane;
-        const uint64_t f = w < W ? Fc[v * W + w] : 0ull;
+        const uint64_t f = w < W && aw_has(AWc, v, w) ? Fc[v * W + w] : 0ull;
         scatter_row<CHURN, K, STORE_E, 0, PART>(g, st, p, L, lane, v, rb, deg, chunk, sl, f, rv, 0, c PROF_PASS);
       }
     };
@@ -1722,6 +1757,9 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
     // UP: the seen row and, in the stage's mask field, the push row (the arrivals)
     if (valid) q.s = ld_once(&(PO ? Fc : st.seen)[(int64_t)q.u * W + lane]);
     if (UP) q.am = valid ? st.next[cur][(int64_t)q.u * W + lane] : 0ull;
+    // PO: the row's active-word mask (a frontier row written by the update may hold stale words
+    // outside it, RoundParams::store_f == 2)
+    if (PO) q.am = ldc(st.AW[cur] + q.u);
     const uint32_t j = q.beg + lane;
     if (j < q.end) {
       if (GATHER) q.v = ld_once(&g.colidx[j]);
@@ -1972,7 +2010,7 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
     activity(cc);
     issue(d);
     PROF_MARK(2);
-    const uint64_t nw = PO ? a.s : acc & need;
+    const uint64_t nw = PO ? ((a.am >> lane) & 1ull ? a.s : 0ull) : acc & need;
     const uint64_t wm = __ballot(nw != 0ull);
     if (!PO && nw) {
       st_frow(&st.seen[u * W + lane], a.s | nw);
@@ -1986,7 +2024,7 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
     }
     if (wm) {
       if (!PO) {
-        if (valid && p.store_f) st_frow(&Fc[u * W + lane], nw);
+        if (valid && p.store_f && (p.store_f != 2 || nw)) st_frow(&Fc[u * W + lane], nw);
         aw |= 1u << (u & 31);
         if (lane == 0) {
           st.AW[cur][u] = wm;
@@ -2456,7 +2494,9 @@ hipError_t launch_gossip_pull(const DevGraph& g, const DevState& st, const Round
   }
   if (fused_pull && st.W <= 64 && st.AW[(p.round & 1) ^ 1] && p.phase < 0) {
     RoundParams pp = p;
-    pp.store_f = 1;  // the sparse push of this round reads the frontier rows
+    // the sparse push of this round reads the frontier rows (its listed words only: whole rows,
+    // or the nonzero words when nobody else can observe them, store_f == 2)
+    pp.store_f = p.store_f == 2 ? 2 : 1;
     // (K = 0: no picks here, and the relay counters take the run's fanout)
     if (hp.n_items)
       launch_hub_partial<false, true>(g, st, pp, hp, s);
@@ -2507,6 +2547,15 @@ static bool update_pair_on() {
   return on;
 }
 
+// 32 < W <= 64 rows: two touched peers per stage of the pipelined update (P2PG_UPDATE_DUAL=0: one)
+static bool update_dual_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("P2PG_UPDATE_DUAL");
+    return !(e && std::strcmp(e, "0") == 0);
+  }();
+  return on;
+}
+
 hipError_t launch_gossip_update(const DevGraph& g, const DevState& st, const RoundParams& p,
                                 hipStream_t s) {
   // blocks cap (P2PG_UPDATE_GRID): c4 A/B, interleaved, update ms per step: 256 / 512 / 1024 /
@@ -2549,9 +2598,11 @@ hipError_t launch_gossip_update(const DevGraph& g, const DevState& st, const Rou
       default: hipLaunchKernelGGL(k_gossip_update_g<5>, dim3(grid), dim3(256), 0, s, g, st, p); break;
     }
   } else if (st.W <= 32 && pipelined && update_pair_on()) {
-    hipLaunchKernelGGL(k_gossip_update1<true>, dim3(grid), dim3(256), 0, s, g, st, p);
+    hipLaunchKernelGGL(k_gossip_update1<2>, dim3(grid), dim3(256), 0, s, g, st, p);
+  } else if (st.W <= 64 && pipelined && update_dual_on()) {
+    hipLaunchKernelGGL(k_gossip_update1<3>, dim3(grid), dim3(256), 0, s, g, st, p);
   } else if (st.W <= 64 && pipelined)
-    hipLaunchKernelGGL(k_gossip_update1<false>, dim3(grid), dim3(256), 0, s, g, st, p);
+    hipLaunchKernelGGL(k_gossip_update1<1>, dim3(grid), dim3(256), 0, s, g, st, p);
   else
     hipLaunchKernelGGL(k_gossip_update, dim3(grid), dim3(256), 0, s, g, st, p);
   return hipGetLastError();
@@ -2690,7 +2741,7 @@ hipError_t launch_gossip_update_push(const DevGraph& g, const DevState& st, cons
     ph.border = g.H;
     ph.phase = 1;
     const int grid = (int)std::min<int64_t>(grid_tasks((g.V + 31) >> 5), 1024);
-    hipLaunchKernelGGL(k_gossip_update1<false>, dim3(grid), dim3(256), 0, s, g, st, ph);
+    hipLaunchKernelGGL(k_gossip_update1<1>, dim3(grid), dim3(256), 0, s, g, st, ph);
     r = hipGetLastError();
     if (r != hipSuccess) return r;
   }

@@ -91,6 +91,7 @@ SIGNATURES = {
     "p2pg_read_planes": (ctypes.c_int, [_P, _P, _P, _P]),
     "p2pg_read_seen_word": (ctypes.c_int, [_P, _I32, _P]),
     "p2pg_kernel_times": (ctypes.c_int, [_P, _P, _P]),
+    "p2pg_set_timed_classes": (ctypes.c_int, [_P, ctypes.c_uint32]),
     "p2pg_set_global_ids": (ctypes.c_int, [_P, _P]),
     "p2pg_set_exchange": (ctypes.c_int, [_P, _I64, _P, _I64, _P]),
     "p2pg_set_ghost_senders": (ctypes.c_int, [_P, _P, _P]),

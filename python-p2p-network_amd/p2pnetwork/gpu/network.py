@@ -326,6 +326,15 @@ class GraphNetwork:
         self._check(_lib.lib().p2pg_kernel_times(self._h, _lib.ptr(ms), _lib.ptr(cnt)))
         return {k: (float(ms[i]), int(cnt[i])) for i, k in enumerate(self.KERNEL_CLASSES)}
 
+    def set_timed_classes(self, classes=None):
+        """Time only these kernel classes with HIP events (None = all; p2pg_set_timed_classes):
+        events cost stream time, so a measurement can bracket its dominant kernel alone."""
+        names = self.KERNEL_CLASSES if classes is None else classes
+        mask = 0
+        for k in names:
+            mask |= 1 << self.KERNEL_CLASSES.index(k)
+        self._check(_lib.lib().p2pg_set_timed_classes(self._h, mask))
+
     # -- vertex-partitioned runs (p2pnetwork.gpu.partition) --------------------------------
     def set_global_ids(self, gid):
         self._gid = np.ascontiguousarray(gid, dtype=np.int32)

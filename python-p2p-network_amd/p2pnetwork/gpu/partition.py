@@ -231,7 +231,7 @@ class PartitionedNetwork:
 
     def __init__(self, graph, world, rank, transport, mode="flood", fanout=3, gossip_seed=0x5EED,
                  churn_threshold_value=0, churn_seed=0xC0FFEE, record=False, timing=False,
-                 device=0, engine_factory=None, overlap=True, deliveries=False):
+                 device=0, engine_factory=None, overlap=True, deliveries=False, msg_id_base=0):
         if not 1 <= world <= MAX_RANKS:
             raise ValueError(f"vertex partition over {world} ranks: the exchange supports 1..{MAX_RANKS}")
         self.world, self.rank, self.transport = world, rank, transport
@@ -249,10 +249,13 @@ class PartitionedNetwork:
         self.overlap = overlap
         self.part = VertexPartition(graph, world, rank)
         make = engine_factory or GraphNetwork
+        # msg_id_base: this job's broadcasts are messages msg_id_base.. of a larger set (a message
+        # split on top of the vertex partition: each group of ranks runs its own share)
+        extra = {"msg_id_base": msg_id_base} if msg_id_base else {}
         self.net = make(self.part.local_graph(), mode=mode, fanout=fanout, gossip_seed=gossip_seed,
                         churn_threshold_value=churn_threshold_value, churn_seed=churn_seed,
                         record=record, timing=timing, device=device, autostop=False,
-                        local_graph=True)
+                        local_graph=True, **extra)
         # device runs: the engine launches on a torch stream of its own, so the receives (torch's
         # current stream, which RCCL orders after its transfers) are ordered before the unpack by
         # a stream wait (_ready), and the next round's interior peers still overlap the transfers
@@ -394,6 +397,9 @@ class PartitionedNetwork:
 
     def kernel_times(self):
         return self.net.kernel_times()
+
+    def set_timed_classes(self, classes=None):
+        self.net.set_timed_classes(classes)
 
     def owned_planes(self):
         """(global ids, seen rows) of the peers this rank owns."""

@@ -25,10 +25,9 @@ def load(path):
 
 
 def short(name):
-    n = name.split("(")[0]
     for p in ("void ", "p2pg::", "(anonymous namespace)::"):
-        n = n.replace(p, "")
-    return n[:60]
+        name = name.replace(p, "")
+    return name.split("(")[0][:60]
 
 
 def main():
@@ -62,6 +61,13 @@ def main():
         gaps.sort(reverse=True)
         for g, x, y in gaps[:top]:
             print(f"   {g / 1e3:8.1f} us  {x}  ->  {y}")
+        by = {}
+        for st, en, nm in seg:
+            k = short(nm)
+            t, n = by.get(k, (0, 0))
+            by[k] = (t + en - st, n + 1)
+        for k, (t, n) in sorted(by.items(), key=lambda x: -x[1][0])[:top]:
+            print(f"   busy {t / 1e6:8.3f} ms in {n:4d}  {k}")
 
 
 if __name__ == "__main__":
