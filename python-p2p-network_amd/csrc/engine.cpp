@@ -128,6 +128,8 @@ struct p2pg_engine {
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
   hipEvent_t ev[2] = {nullptr, nullptr};
+  hipEvent_t ev_sync = nullptr;  // round_sync's marker (no timing)
+  bool spin = false;             // round_sync polls the marker instead of blocking (P2PG_SPIN)
   // per-launch timing events: recorded around each launch, resolved after the round's stream
   // sync (no extra host synchronisation inside a round)
   std::vector<hipEvent_t> ev_pool;
@@ -318,6 +320,20 @@ DevGraph graph_for_arrivals(const p2pg_engine* e, int32_t r) {
   return graph(e);
 }
 
+// The host's wait for a round's counters (everything enqueued on the engine's stream so far):
+// a blocking stream synchronisation, or -- P2PG_SPIN -- a marker event polled in a loop, which
+// trades a spinning host thread for the wake-up latency of a blocking wait (the GPU idles
+// between a round's counter copy and the next round's first launch for as long as the host takes
+// to notice).
+hipError_t round_sync(p2pg_engine* e) {
+  if (!e->spin) return hipStreamSynchronize(e->stream);
+  hipError_t r = hipEventRecord(e->ev_sync, e->stream);
+  if (r != hipSuccess) return r;
+  while ((r = hipEventQuery(e->ev_sync)) == hipErrorNotReady) {
+  }
+  return r;
+}
+
 // Timed launch: kernel class cls in [0, P2PG_KCLASS_N) (see include/p2pgpu.h).
 template <class F>
 int timed(p2pg_engine* e, int cls, F&& launch) {
@@ -428,6 +444,10 @@ bool predict_dense(const p2pg_engine* e) {
 // half of v_thresh * v_conn).  Only the push form depends on it, never a result.
 bool clearly_sparse(const p2pg_engine* e) {
   if (e->round == 0) return false;  // (origination: the counters are the host's)
+  // a bound, not a guess: every active peer of this round received at least one of the masks
+  // pushed in the last one (prev_sw), and a dense round needs v_thresh * v_conn active peers
+  // (c4: rounds 5 and 6, whose frontiers grow too fast for the guess below)
+  if (e->prev_sw > 0 && (double)e->prev_sw < e->v_thresh * (double)e->v_conn) return true;
   if (e->saw_dense) return e->last_new < e->prev2_new;
   if (e->prev_av == 0) return true;  // nothing arrives: an empty round
   const double grow = e->prev2_av ? std::max(1.0, (double)e->prev_av / (double)e->prev2_av) : 64.0;
@@ -611,6 +631,8 @@ int p2pg_create(const p2pg_config* cfg, p2pg_engine** out) {
   e->stream = e->own_stream;
   HIPCHK(e, hipEventCreate(&e->ev[0]));
   HIPCHK(e, hipEventCreate(&e->ev[1]));
+  HIPCHK(e, hipEventCreateWithFlags(&e->ev_sync, hipEventDisableTiming));
+  if (const char* f = std::getenv("P2PG_SPIN")) e->spin = std::strcmp(f, "0") != 0;
   HIPCHK(e, hipHostMalloc((void**)&e->h_stats, STAT_BYTES));
   *out = e;
   return P2PG_OK;
@@ -994,7 +1016,7 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
   uint64_t tot[STAT_N] = {0};
   auto read_stats = [&]() -> int {
     HIPCHK(e, hipMemcpyAsync(e->h_stats, s.stats, STAT_BYTES, hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(e, hipStreamSynchronize(e->stream));
+    HIPCHK(e, round_sync(e));
     int r2 = resolve_timings(e);
     if (r2) return r2;
     for (int i = 0; i < STAT_N; ++i) tot[i] = 0;
@@ -1041,12 +1063,13 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
       have_tot = true;
     }
     // decay phase (fewer first receipts than the round before): most pushes are duplicates,
-    // so the sparse push drops seen bits before its atomics (RoundParams::dedup_push; without
-    // this round's counters: the phase of the rounds before)
+    // so the sparse push drops seen bits before its atomics (RoundParams::dedup_push).  The
+    // phase is "after the dense rounds" (saw_dense), a fact every schedule agrees on -- a
+    // batched decay round, a blind push and a round that read its counters first must filter
+    // alike, because the filter decides which fully-seen masks are still pushed, i.e. the
+    // touched-words counter of the next round (results never depend on it)
     if (!use_e && sparse_scatter_on(e))
-      p.dedup_push = e->push_dedup == 1 ||
-                     (e->push_dedup < 0 && (have_tot ? tot[ST_NEW] < e->last_new
-                                                     : e->saw_dense && e->last_new < e->prev2_new));
+      p.dedup_push = e->push_dedup == 1 || (e->push_dedup < 0 && e->saw_dense);
     const uint64_t list_words = have_tot ? tot[ST_ACTIVE_W] : e->prev_sw;
     if ((rc = timed(e, use_e ? 6 : 2, [&] {
            return use_e ? launch_gossip_scatter(g, s, p, e->d_hub, e->n_hub, true, e->stream,
@@ -1176,7 +1199,7 @@ static int run_decay_batch(p2pg_engine* e, int32_t R, p2pg_round_stats* out, int
     partial[i] = p.store_f == 2;
     rc = timed(e, 4, [&] { return launch_gossip_update(g, s, p, e->stream); });
     if (rc == P2PG_OK && s.hop) rc = timed(e, 3, [&] { return launch_record(g, s, p, e->stream); });
-    p.dedup_push = e->push_dedup != 0;  // decay phase
+    p.dedup_push = e->push_dedup != 0;  // decay phase (saw_dense: the rule of p2pg_step)
     if (rc == P2PG_OK)
       rc = timed(e, 2, [&] {
         return launch_scatter_atomic(e, g, p, std::min<uint64_t>(e->prev_sw, words));
@@ -1187,7 +1210,7 @@ static int run_decay_batch(p2pg_engine* e, int32_t R, p2pg_round_stats* out, int
   if (rc) return rc;
   HIPCHK(e, hipMemcpyAsync(e->h_bstats, e->d_bstats, sizeof(unsigned long long) * SLOT * R,
                            hipMemcpyDeviceToHost, e->stream));
-  HIPCHK(e, hipStreamSynchronize(e->stream));
+  HIPCHK(e, round_sync(e));
   if ((rc = resolve_timings(e))) return rc;
   *ran = 0;
   for (int32_t i = 0; i < R; ++i) {
@@ -1957,6 +1980,7 @@ void p2pg_destroy(p2pg_engine* e) {
   for (int i = 0; i < 2; ++i)
     if (e->ev[i]) (void)hipEventDestroy(e->ev[i]);
   for (hipEvent_t ev : e->ev_pool) (void)hipEventDestroy(ev);
+  if (e->ev_sync) (void)hipEventDestroy(e->ev_sync);
   if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
   delete e;
 }

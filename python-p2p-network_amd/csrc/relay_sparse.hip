@@ -124,27 +124,30 @@ __global__ __launch_bounds__(256) void k_sparse_words(DevGraph g, DevState st, R
 }
 
 // Exclusive prefix sum of the chunk counts (one block): chunk_off, and the total into *count.
-// Tiles of 1024 x 8 counts: a thread's 8 consecutive counts arrive in two 16 B loads, so a
-// tile costs one memory trip (a per-thread serial range cost ~20 trips: 26 us per launch).
+// Tiles of 1024 x CPT counts: a thread's CPT consecutive counts arrive in CPT / 4 16 B loads, so a
+// tile costs one memory trip, and one tile covers config 4's 19.5K chunks (8 counts per thread
+// took three dependent tiles, 14 us per launch; a per-thread serial range ~20 trips, 26 us).
+constexpr int CPT = 24;
 __global__ __launch_bounds__(1024) void k_chunk_scan(int64_t n, SparseBufs b) {
   __shared__ uint64_t wsum[16];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   uint64_t carry = 0;
-  for (int64_t tile = 0; tile < n; tile += 8192) {
-    const int64_t i0 = tile + 8 * (int64_t)t;
-    uint32_t c[8];
-    if (i0 + 8 <= n) {  // chunk_cnt is 16 B aligned
-      const uint4 a = *reinterpret_cast<const uint4*>(b.chunk_cnt + i0);
-      const uint4 d = *reinterpret_cast<const uint4*>(b.chunk_cnt + i0 + 4);
-      c[0] = a.x; c[1] = a.y; c[2] = a.z; c[3] = a.w;
-      c[4] = d.x; c[5] = d.y; c[6] = d.z; c[7] = d.w;
+  for (int64_t tile = 0; tile < n; tile += 1024 * CPT) {
+    const int64_t i0 = tile + CPT * (int64_t)t;
+    uint32_t c[CPT];
+    if (i0 + CPT <= n) {  // chunk_cnt is 16 B aligned, CPT a multiple of 4
+#pragma unroll
+      for (int j = 0; j < CPT; j += 4) {
+        const uint4 a = *reinterpret_cast<const uint4*>(b.chunk_cnt + i0 + j);
+        c[j] = a.x; c[j + 1] = a.y; c[j + 2] = a.z; c[j + 3] = a.w;
+      }
     } else {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) c[j] = i0 + j < n ? b.chunk_cnt[i0 + j] : 0u;
+      for (int j = 0; j < CPT; ++j) c[j] = i0 + j < n ? b.chunk_cnt[i0 + j] : 0u;
     }
     uint64_t s = 0;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) s += c[j];
+    for (int j = 0; j < CPT; ++j) s += c[j];
     // block exclusive scan of s: wave scans (64-bit shuffles), then the 16 wave totals
     uint64_t x = s;
 #pragma unroll
@@ -162,7 +165,7 @@ __global__ __launch_bounds__(1024) void k_chunk_scan(int64_t n, SparseBufs b) {
     __syncthreads();  // wsum is rewritten by the next tile
     uint64_t run = before + x - s;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < CPT; ++j) {
       if (i0 + j < n) b.chunk_off[i0 + j] = run;
       run += c[j];
     }

@@ -302,7 +302,8 @@ def test_run_chunks_keep_the_last_frontier(M, monkeypatch):
     plane as round-by-round stepping (W = 64: one peer per wave; W = 8: grouped kernel)."""
     from p2pnetwork.gpu import GraphNetwork, PeerGraph, make_sources
     monkeypatch.setenv("P2PG_V_THRESH", "0.3")  # dense rounds from 30 % active peers on
-    g = PeerGraph.barabasi_albert(200_000, 4, seed=3)
+    # (W = 64 on 100K peers: each cut compares a whole round's delivery stream, up to ~10^8 records)
+    g = PeerGraph.barabasi_albert(100_000 if M > 512 else 200_000, 4, seed=3)
     src = make_sources(g.V, M, seed=3)
     with GraphNetwork(g, mode="gossip", fanout=3, gossip_seed=GSEED) as a, \
             GraphNetwork(g, mode="gossip", fanout=3, gossip_seed=GSEED) as b:
