@@ -479,6 +479,20 @@ bool partial_frontier(const p2pg_engine* e, bool skip) {
          e->partial_f;
 }
 
+// A fused dense round (pull of E[(r-1)&1] + pushes into E[r&1]) and its hub pushes.
+hipError_t launch_fused_round(p2pg_engine* e, const DevGraph& g, const RoundParams& p) {
+  DevState& s = e->st;
+  if (e->d_gid) {  // the exchanged row pushes it ORed in are cleared after the pass
+    hipError_t r = launch_gossip_fused(g, s, p, e->hp, nullptr, 0, true, e->stream);
+    return r != hipSuccess ? r : launch_clear_arrivals(s, p.round, e->V, e->stream);
+  }
+  const bool wa = wide_atomic_on(e);
+  hipError_t r = launch_gossip_fused(g, s, p, e->hp, e->d_hub_big, e->n_hub_big, wa, e->stream);
+  if (r != hipSuccess || !wa) return r;
+  return launch_wide_push_e(g, s, p, e->d_hub_big, e->n_hub_big, e->d_wide_big, e->n_wide_big,
+                            e->stream);
+}
+
 // Can this vertex-partitioned rank (global ids set) take the dense rounds (E pushes, fused and
 // pull-only passes in their PART form, relay_kernels.hip)?  Packed rows over 16 < W <= 64 and
 // two E planes; otherwise its gossip pushes go by row atomics only.
@@ -975,19 +989,7 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
       // a frontier nobody observes is not stored: inside p2pg_run (not its last allowed
       // round), without hop/parent records
       p.store_f = (e->skip_frontier && !s.hop) ? 0 : 1;
-      if ((rc = timed(e, 7, [&] {
-             if (part) {  // the exchanged row pushes it ORed in are cleared after the pass
-               hipError_t r = launch_gossip_fused(g, s, p, e->hp, nullptr, 0, true, e->stream);
-               return r != hipSuccess ? r : launch_clear_arrivals(s, p.round, e->V, e->stream);
-             }
-             const bool wa = wide_atomic_on(e);
-             hipError_t r = launch_gossip_fused(g, s, p, e->hp, e->d_hub_big, e->n_hub_big, wa,
-                                                e->stream);
-             if (r != hipSuccess || !wa) return r;
-             return launch_wide_push_e(g, s, p, e->d_hub_big, e->n_hub_big, e->d_wide_big,
-                                       e->n_wide_big, e->stream);
-           })))
-        return rc;
+      if ((rc = timed(e, 7, [&] { return launch_fused_round(e, g, p); }))) return rc;
     } else {
       if ((rc = timed(e, 5, [&] {
              hipError_t r = launch_gossip_pull(g, s, p, e->hp, e->stream);
