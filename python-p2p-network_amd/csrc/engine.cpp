@@ -163,6 +163,15 @@ struct p2pg_engine {
   unsigned long long* h_bstats = nullptr;  // pinned
   int batch_rounds = -1;        // P2PG_RUN_BATCH (rounds per host synchronisation in the decay
                                 // phase; 1 = none), -1 = the default
+  // Double-buffered seen plane: a reset swaps in the spare (zeroed earlier) and zeroes the plane
+  // it replaces on a side stream, behind the work already queued -- the zeroing overlaps the next
+  // run's first rounds (latency-bound sparse rounds) instead of leading it.  P2PG_SEEN_SPARE=0,
+  // or a failed allocation of the spare: the reset zeroes seen in stream order.
+  bool seen_spare_on = true;
+  uint64_t* seen_spare = nullptr;
+  bool spare_pending = false;   // a zeroing of seen_spare is queued on `side` (ev_spare marks it)
+  hipStream_t side = nullptr;
+  hipEvent_t ev_spare = nullptr, ev_main = nullptr;
 };
 
 namespace {
@@ -193,6 +202,11 @@ void dfree(T*& p) {
 void free_state(p2pg_engine* e) {
   DevState& s = e->st;
   dfree(s.seen);
+  if (e->seen_spare) {
+    if (e->spare_pending) (void)hipStreamSynchronize(e->side);
+    dfree(e->seen_spare);
+  }
+  e->spare_pending = false;
   for (int i = 0; i < 2; ++i) {
     dfree(s.F[i]);
     dfree(s.next[i]);
@@ -638,6 +652,7 @@ int p2pg_create(const p2pg_config* cfg, p2pg_engine** out) {
   if (const char* f = std::getenv("P2PG_RUN_BATCH")) e->batch_rounds = std::atoi(f);
   if (const char* f = std::getenv("P2PG_DECAY_PRED")) e->decay_pred = std::strcmp(f, "0") != 0;
   if (const char* f = std::getenv("P2PG_PARTIAL_F")) e->partial_f = std::strcmp(f, "0") != 0;
+  if (const char* f = std::getenv("P2PG_SEEN_SPARE")) e->seen_spare_on = std::strcmp(f, "0") != 0;
   if (const char* m = std::getenv("P2PG_GOSSIP_PUSH"))
     e->push_mode = !std::strcmp(m, "atomic") ? 1 : (!std::strcmp(m, "store") ? 2 : 0);
   HIPCHK(e, hipSetDevice(cfg->device));
@@ -833,11 +848,58 @@ int p2pg_set_sources(p2pg_engine* e, int32_t M, const int32_t* src) {
   return p2pg_reset(e);
 }
 
+}  // extern "C"
+
+namespace {
+
+// p2pg_reset's spare seen plane (p2pg_engine::seen_spare): allocated on first use; false when
+// disabled or when the device has no room for it (then it stays disabled)
+bool spare_ready(p2pg_engine* e) {
+  if (!e->seen_spare_on) return false;
+  if (e->seen_spare) return true;
+  if (!e->side) {
+    if (hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&e->ev_spare, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&e->ev_main, hipEventDisableTiming) != hipSuccess) {
+      (void)hipGetLastError();
+      e->seen_spare_on = false;
+      return false;
+    }
+  }
+  if (hipMalloc((void**)&e->seen_spare, e->plane_bytes) != hipSuccess) {
+    (void)hipGetLastError();
+    e->seen_spare = nullptr;
+    e->seen_spare_on = false;
+    return false;
+  }
+  e->spare_pending = false;
+  return true;
+}
+
+}  // namespace
+
+extern "C" {
+
 int p2pg_reset(p2pg_engine* e) {
   if (!e || !e->have_state) return fail(e, P2PG_ERR_STATE, "reset: no sources set");
   HIPCHK(e, hipSetDevice(e->cfg.device));
   DevState& s = e->st;
-  HIPCHK(e, hipMemsetAsync(s.seen, 0, e->plane_bytes, e->stream));
+  if (!spare_ready(e)) {
+    HIPCHK(e, hipMemsetAsync(s.seen, 0, e->plane_bytes, e->stream));
+  } else {
+    if (e->spare_pending) {  // the spare is zero once the side stream's zeroing has run
+      HIPCHK(e, hipStreamWaitEvent(e->stream, e->ev_spare, 0));
+      std::swap(s.seen, e->seen_spare);
+    } else {  // (first reset with a spare: zero the plane in use here, the spare below)
+      HIPCHK(e, hipMemsetAsync(s.seen, 0, e->plane_bytes, e->stream));
+    }
+    // the replaced plane: zeroed on the side stream after everything queued so far has read it
+    HIPCHK(e, hipEventRecord(e->ev_main, e->stream));
+    HIPCHK(e, hipStreamWaitEvent(e->side, e->ev_main, 0));
+    HIPCHK(e, hipMemsetAsync(e->seen_spare, 0, e->plane_bytes, e->side));
+    HIPCHK(e, hipEventRecord(e->ev_spare, e->side));
+    e->spare_pending = true;
+  }
   HIPCHK(e, hipMemsetAsync(s.S, 0, e->bm_bytes, e->stream));
   for (int i = 0; i < 2; ++i) HIPCHK(e, hipMemsetAsync(s.A[i], 0, e->bm_bytes, e->stream));
   if (s.next[0] && ((!e->done && e->round > 0) || e->consume_next)) {
@@ -1983,6 +2045,9 @@ void p2pg_destroy(p2pg_engine* e) {
     if (e->ev[i]) (void)hipEventDestroy(e->ev[i]);
   for (hipEvent_t ev : e->ev_pool) (void)hipEventDestroy(ev);
   if (e->ev_sync) (void)hipEventDestroy(e->ev_sync);
+  if (e->ev_spare) (void)hipEventDestroy(e->ev_spare);
+  if (e->ev_main) (void)hipEventDestroy(e->ev_main);
+  if (e->side) (void)hipStreamDestroy(e->side);
   if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
   delete e;
 }
