@@ -181,7 +181,7 @@ def cpu_model():
 
 def cpu_baseline(g, w, src, sample_msgs, thr, object_seconds=10.0):
     """Two CPU legs on a bounded sample of the same workload (reported, not a target):
-    (ii) the C oracle (oracle/relay_oracle.c, OpenMP, every host thread) on the same graph with
+    (ii) the C oracle (oracle/relay_oracle.c, OpenMP, every core of the job's affinity set) on the same graph with
     the first `sample_msgs` broadcasts -- the headline cpu_baseline value; (i) the 1-core,
     object-level Python relay (oracle/object_relay.py: Node / NodeConnection-shaped objects, JSON
     + EOT framing per send, the reference's per-relay work) on broadcast 0 until ~object_seconds
@@ -215,6 +215,9 @@ def cpu_baseline(g, w, src, sample_msgs, thr, object_seconds=10.0):
                        f"1 Python thread, {len(sim.peers)} peer objects)"}
     out = dict(c_leg)
     out["cpu_model"] = cpu_model()
+    # the job's CPU share: a GPU box pins a one-GPU job to its slice of the host
+    out["affinity_cores"] = len(os.sched_getaffinity(0))
+    out["host_cpus"] = os.cpu_count()
     out["legs"] = {"c_openmp": c_leg, "python_objects_1core": o_leg}
     return out
 

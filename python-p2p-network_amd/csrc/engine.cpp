@@ -166,7 +166,8 @@ struct p2pg_engine {
   // Double-buffered seen plane: a reset swaps in the spare (zeroed earlier) and zeroes the plane
   // it replaces on a side stream, behind the work already queued -- the zeroing overlaps the next
   // run's first rounds (latency-bound sparse rounds) instead of leading it.  P2PG_SEEN_SPARE=0,
-  // or a failed allocation of the spare: the reset zeroes seen in stream order.
+  // a plane above 1/16 of the device or a failed allocation: the reset zeroes seen in stream
+  // order (spare_ready).
   bool seen_spare_on = true;
   uint64_t* seen_spare = nullptr;
   bool spare_pending = false;   // a zeroing of seen_spare is queued on `side` (ev_spare marks it)
@@ -857,6 +858,16 @@ namespace {
 bool spare_ready(p2pg_engine* e) {
   if (!e->seen_spare_on) return false;
   if (e->seen_spare) return true;
+  // only where it is cheap: a plane of at most 1/16 of the device (config 4: 5.1 GB of 288) with
+  // room to spare, so that the copy never takes the memory a larger run (config 5's 51 GB planes,
+  // several engines of one process) needs
+  size_t free_b = 0, total_b = 0;
+  if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || e->plane_bytes > total_b / 16 ||
+      free_b < 4 * e->plane_bytes) {
+    (void)hipGetLastError();
+    e->seen_spare_on = false;
+    return false;
+  }
   if (!e->side) {
     if (hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&e->ev_spare, hipEventDisableTiming) != hipSuccess ||

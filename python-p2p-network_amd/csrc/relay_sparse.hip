@@ -124,38 +124,36 @@ __global__ __launch_bounds__(256) void k_sparse_words(DevGraph g, DevState st, R
 }
 
 // Exclusive prefix sum of the chunk counts (one block): chunk_off, and the total into *count.
-// Tiles of 1024 x CPT counts: a thread's CPT consecutive counts arrive in CPT / 4 16 B loads, so a
-// tile costs one memory trip, and one tile covers config 4's 19.5K chunks (8 counts per thread
-// took three dependent tiles, 14 us per launch; a per-thread serial range ~20 trips, 26 us).
+// Tiles of 16 waves x 64 lanes x CPT counts; wave v scans its contiguous 64 * CPT counts as CPT
+// rows of 64 (lane = count: 16 B-per-lane loads and 8 B-per-lane stores, every row one 256 B /
+// 512 B contiguous access), then the 16 wave totals offset the waves.  One tile covers config
+// 4's 19.5K chunks.  (Thread-major runs -- CPT consecutive counts per thread -- left every store
+// instruction 64 partial lines apart: 13 us per launch, a fixed cost of every sparse round.)
+// Row sums within a wave's segment stay 32-bit: <= 64 * CPT chunks x SW_TASKS * 32 peers x 64
+// words < 2^32.
 constexpr int CPT = 24;
+static_assert((uint64_t)64 * CPT * SW_TASKS * 32 * 64 < (1ull << 32), "32-bit segment sums");
 __global__ __launch_bounds__(1024) void k_chunk_scan(int64_t n, SparseBufs b) {
   __shared__ uint64_t wsum[16];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   uint64_t carry = 0;
-  for (int64_t tile = 0; tile < n; tile += 1024 * CPT) {
-    const int64_t i0 = tile + CPT * (int64_t)t;
+  for (int64_t tile = 0; tile < n; tile += 16 * 64 * CPT) {
+    const int64_t s0 = tile + (int64_t)wv * 64 * CPT + lane;
     uint32_t c[CPT];
-    if (i0 + CPT <= n) {  // chunk_cnt is 16 B aligned, CPT a multiple of 4
 #pragma unroll
-      for (int j = 0; j < CPT; j += 4) {
-        const uint4 a = *reinterpret_cast<const uint4*>(b.chunk_cnt + i0 + j);
-        c[j] = a.x; c[j + 1] = a.y; c[j + 2] = a.z; c[j + 3] = a.w;
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < CPT; ++j) c[j] = i0 + j < n ? b.chunk_cnt[i0 + j] : 0u;
+    for (int j = 0; j < CPT; ++j) {  // all loads first
+      const int64_t i = s0 + 64 * j;
+      c[j] = i < n ? b.chunk_cnt[i] : 0u;
     }
-    uint64_t s = 0;
+    uint32_t x[CPT];  // exclusive offsets within the wave's segment
+    uint32_t run = 0;
 #pragma unroll
-    for (int j = 0; j < CPT; ++j) s += c[j];
-    // block exclusive scan of s: wave scans (64-bit shuffles), then the 16 wave totals
-    uint64_t x = s;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint64_t y = __shfl_up(x, o);
-      if (lane >= o) x += y;
+    for (int j = 0; j < CPT; ++j) {
+      const uint32_t inc = wave_scan_u32(c[j]);
+      x[j] = run + inc - c[j];
+      run += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
     }
-    if (lane == 63) wsum[wv] = x;
+    if (lane == 0) wsum[wv] = run;
     __syncthreads();
     uint64_t before = carry, all = carry;
     for (int i = 0; i < 16; ++i) {
@@ -163,11 +161,10 @@ __global__ __launch_bounds__(1024) void k_chunk_scan(int64_t n, SparseBufs b) {
       all += wsum[i];
     }
     __syncthreads();  // wsum is rewritten by the next tile
-    uint64_t run = before + x - s;
 #pragma unroll
     for (int j = 0; j < CPT; ++j) {
-      if (i0 + j < n) b.chunk_off[i0 + j] = run;
-      run += c[j];
+      const int64_t i = s0 + 64 * j;
+      if (i < n) b.chunk_off[i] = before + x[j];
     }
     carry = all;
   }
