@@ -148,6 +148,32 @@ def test_partitioned_engines_match_single_gpu(kind, mode, M, thr, world, overlap
     np.testing.assert_array_equal(par1, ora.parent)
 
 
+# Every origin inside the LAST rank's id block (Watts-Strogatz: the other ranks are reached late,
+# only through exchanged rows): a rank's own pushed-mask count then says nothing about the frontier
+# the exchange hands it, so a partitioned rank never pushes blind and sizes its (peer, word) list
+# by its own counters (advisor, round 4).  Narrow rows (row atomics only on partitioned ranks) and
+# the packed dense form, with churn.
+@pytest.mark.parametrize("M,world,thr", [(1024, 2, 0), (4096, 3, 300_000_000)])
+def test_partitioned_gossip_sources_in_one_block(M, world, thr):
+    from p2pnetwork.gpu import GraphNetwork, VertexPartition
+    g = graph("ws")
+    bounds = VertexPartition.ranges(g, world)
+    lo, hi = int(bounds[world - 1]), int(bounds[world])
+    rng = np.random.default_rng(5)
+    src = rng.integers(lo, hi, size=M).astype(np.int32)
+    kw = dict(mode="gossip", fanout=3, gossip_seed=31, churn_threshold_value=thr, churn_seed=8)
+    res = run_partitioned(g, world, src, **kw)
+    with GraphNetwork(g, **kw) as one:
+        one.broadcast(src)
+        rounds1 = one.run()
+        seen1 = one.seen_plane()
+    np.testing.assert_array_equal(assemble(res, g.V, (M + 63) // 64), seen1)
+    for rounds, *_ in res:
+        for k in ("new_deliveries", "relays", "active_vertices", "active_words"):
+            np.testing.assert_array_equal(trim_zeros([getattr(r, k) for r in rounds]),
+                                          trim_zeros([getattr(r, k) for r in rounds1]), err_msg=k)
+
+
 # Partitioned ranks take gossip's dense rounds at 16 < W <= 64 (relay_kernels.hip PART kernels):
 # E planes for local connections, row pushes for ghost connections (exchanged as plane 1) ORed
 # into the gather of the next round.  Widths 24 / 32 (two slots per gather load) / 64, the engine's
