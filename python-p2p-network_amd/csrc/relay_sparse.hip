@@ -56,6 +56,10 @@ __device__ __forceinline__ int pass_owner(uint32_t* own, int lane, uint32_t pos,
 #define P2PG_SW_TASKS 16
 #endif
 constexpr int SW_TASKS = P2PG_SW_TASKS;
+#ifndef P2PG_SPARSE_GRID_MAX
+#define P2PG_SPARSE_GRID_MAX 8192
+#endif
+constexpr int64_t SPARSE_GRID_MAX = P2PG_SPARSE_GRID_MAX;
 
 template <bool WRITE>
 __global__ __launch_bounds__(256) void k_sparse_words(DevGraph g, DevState st, RoundParams p,
@@ -442,11 +446,17 @@ hipError_t launch_gossip_scatter_sparse(const DevGraph& g, const DevState& st,
                                         const SparseBufs& b, hipStream_t s) {
   if (!gossip_scatter_sparse_supported(st) || b.cap < 1) return hipErrorInvalidValue;
   const int64_t chunks = sparse_chunks(g.V);
-  const int wgrid = grid_tasks(chunks);
+  // up to 8192 blocks (32 waves per CU over a launch; grid_max() is 2048): the push waits on its
+  // atomics' round trips, and 4x the waves in flight took the sparse class 15.5 -> 14.9 ms per
+  // c4 step (profiles/r05/ab_grid_max.txt, _r05u)
+  auto sgrid = [](int64_t tasks) {
+    return (int)std::min<int64_t>(grid_tasks_uncapped(tasks), (int64_t)SPARSE_GRID_MAX);
+  };
+  const int wgrid = sgrid(chunks);
   hipLaunchKernelGGL(k_sparse_words<false>, dim3(wgrid), dim3(256), 0, s, g, st, p, b);
   hipLaunchKernelGGL(k_chunk_scan, dim3(1), dim3(1024), 0, s, chunks, b);
   hipLaunchKernelGGL(k_sparse_words<true>, dim3(wgrid), dim3(256), 0, s, g, st, p, b);
-  const int grid = grid_tasks((expect + 63) >> 6);  // 64 listed words per wave pass
+  const int grid = sgrid((expect + 63) >> 6);  // 64 listed words per wave pass
   const bool ch = p.churn_thr != 0;
 #define P2PG_SPARSE(CH, KK) \
   hipLaunchKernelGGL((k_sparse_push<CH, KK>), dim3(grid), dim3(256), 0, s, g, st, p, b)
