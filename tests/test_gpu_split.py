@@ -29,10 +29,12 @@ def _sum_rounds(parts):
     return [{k: sum(getattr(p[i], k) for p in parts if i < len(p)) for k in ADDITIVE} for i in range(n)]
 
 
-def _check_split(g, M, world, churn=0, bounds=None):
+def _check_split(g, M, world, churn=0, bounds=None, one=None):
+    """one: the single-engine (rounds, seen columns) of these sources, if already run."""
     from p2pnetwork.gpu import make_sources
     src = make_sources(g.V, M, seed=1)
-    full, cols = _run(g, src, 0, churn_threshold_value=churn, churn_seed=0xC0FFEE)
+    full, cols = one if one is not None else _run(g, src, 0, churn_threshold_value=churn,
+                                                  churn_seed=0xC0FFEE)
     parts = []
     bounds = bounds or [r * M // world for r in range(world + 1)]
     for r in range(len(bounds) - 1):
@@ -68,10 +70,20 @@ def test_message_split_union_with_churn_and_ragged_words():
                  bounds=[0, 1024, 1984, 2129])
 
 
+@pytest.fixture(scope="module")
+def c4_one():
+    """Config 4's graph and its one-engine run (rounds, 64 seen columns), shared by the three
+    split sizes (one graph generation and one reference run instead of three)."""
+    from p2pnetwork.gpu import PeerGraph, make_sources
+    g = PeerGraph.barabasi_albert(10_000_000, 4, seed=1)
+    src = make_sources(g.V, 4096, seed=1)
+    return g, _run(g, src, 0, churn_threshold_value=0, churn_seed=0xC0FFEE)
+
+
 @pytest.mark.parametrize("world", [2, 4, 8])
-def test_message_split_config4_full_size(world):
+def test_message_split_config4_full_size(world, c4_one):
     """Config 4 itself (10M-peer BA m=4, 4096 gossips, k=3) as the 2- / 4- / 8-GPU jobs run it:
     the W = 32 / 16 / 8 shares (HALF-mode fused kernel, grouped kernels) union to the one-engine
     run, word for word and counter for counter."""
-    from p2pnetwork.gpu import PeerGraph
-    _check_split(PeerGraph.barabasi_albert(10_000_000, 4, seed=1), 4096, world)
+    g, one = c4_one
+    _check_split(g, 4096, world, one=one)

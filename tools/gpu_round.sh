@@ -7,7 +7,7 @@ tag=${1:?usage: bash tools/gpu_round.sh <tag>}
 mkdir -p gpurun_out/$tag
 export TMPDIR=/tmp
 if [ -z "$SKIP_SUITE" ]; then
-  timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 700 --timeout-method thread -p no:cacheprovider > gpurun_out/$tag/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/$tag/pytest_gpu.log; exit 1; }
+  timeout -k 10 1000 python -u -m pytest tests -m gpu -v --durations=30 --timeout 700 --timeout-method thread -p no:cacheprovider > gpurun_out/$tag/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/$tag/pytest_gpu.log; exit 1; }
   tail -1 gpurun_out/$tag/pytest_gpu.log
 fi
 timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/$tag/bench_c4.json 2> gpurun_out/$tag/bench_c4.err || { tail -20 gpurun_out/$tag/bench_c4.err; exit 1; }
