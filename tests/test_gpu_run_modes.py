@@ -80,3 +80,26 @@ def test_batched_and_blind_rounds_equal_round_by_round(kind, thr, monkeypatch):
     np.testing.assert_array_equal(seen_a, ora.seen)
     want = [tuple(r[f] for f in FIELDS[:-1]) for r in ora.rounds]
     assert [x[:-1] for x in _rows(a)][:len(want)] == want
+
+
+def test_new_sources_and_resets_recount_round_zero():
+    """Round 0's counters come from the host copy of the sources (cached per sources and graph,
+    engine.cpp seed_stats): a second broadcast() with other sources on the same engine, and a
+    reset between runs (the double-buffered seen plane swaps in its zeroed spare), give exactly a
+    fresh engine's rounds -- counters and seen plane -- each time."""
+    from p2pnetwork.gpu import PeerGraph, make_sources
+    g = PeerGraph.barabasi_albert(300_000, 4, seed=11)
+    a, b = make_sources(g.V, 4096, seed=1), make_sources(g.V, 1000, seed=2)
+    ref = {}
+    for name, src in (("a", a), ("b", b)):
+        with _net(g, 0) as net:
+            net.broadcast(src)
+            ref[name] = (_rows(net.run()), net.seen_plane())
+    with _net(g, 0) as net:
+        for name, src in (("a", a), ("b", b), ("a", a)):
+            net.broadcast(src)
+            for _ in range(2):
+                net.reset()
+                rows = _rows(net.run())
+                assert rows == ref[name][0], name
+                np.testing.assert_array_equal(net.seen_plane(), ref[name][1], err_msg=name)
