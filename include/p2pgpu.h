@@ -20,6 +20,13 @@
  *   p2pg_round_stats.relays       <- sum over peers of Node.message_count_send (node.py:65,116)
  *   p2pg_get_new_deliveries       <- the node_message(node, data) events of one round, as
  *                                    (peer, msg, hop, parent) records (node.py:334-338)
+ *   p2pg_get_sends                <- every Node.send_to_node call of one round (node.py:114-120),
+ *                                    i.e. every packet NodeConnection.run hands to node_message
+ *                                    the next round (nodeconnection.py:211-216), duplicates
+ *                                    included, with the ones churn loses (nodeconnection.py:123-126)
+ *   p2pg_drop_relays              <- an app whose node_message did not call send_to_nodes for a
+ *                                    first receipt (README.md:20: the app decides)
+ *   p2pg_round_stats.received     <- sum over peers of message_count_recv (nodeconnection.py:215)
  *   p2pg_read_planes              <- each app's "seen" set + first-receipt (hop, sender)
  *   p2pg_last_error               <- (reference swallows errors via debug_print, node.py:80-83)
  *
@@ -92,6 +99,10 @@ typedef struct p2pg_round_stats {
   uint64_t touched_words;    /* gossip: nonzero pushed-to words consumed in round r       */
   int32_t push_form;         /* gossip: how round r's pushes left (P2PG_PUSH_*); flood 0    */
   int32_t reserved_;
+  uint64_t received;         /* packets that arrived in round r: the sends of round r-1 less
+                                those lost to churn or to a connection removed in between
+                                (sum over peers of message_count_recv += 1,
+                                nodeconnection.py:215; duplicates included, 0 at round 0)  */
 } p2pg_round_stats;
 
 /* ---- graphs (host side; no GPU needed) ---------------------------------------------- */
@@ -143,6 +154,25 @@ int p2pg_run(p2pg_engine* e, int32_t max_rounds, p2pg_round_stats* per_round,
  * the restored engine runs report their deliveries as usual).                              */
 int p2pg_get_new_deliveries(p2pg_engine* e, int64_t cap, int32_t* peer, int32_t* msg,
                             int32_t* hop, int32_t* parent, int64_t* n_out);
+/* Every send of the most recent round -- the send_to_node calls its first receipts made
+ * (node.py:114-120): flood, each connection but the one the receipt came from (all of them at
+ * the origin, node.py:106-112); gossip, the k Philox picks -- as (sender, receiver, msg) records
+ * sorted by (receiver, sender, msg), lost[i] = 1 if the send never arrives (churn drops it,
+ * nodeconnection.py:123-126).  These are exactly the packets the next round's receivers hand to
+ * node_message (nodeconnection.py:211-216), duplicates included; a p2pg_update_edges after this
+ * call loses the ones on removed connections as well.  Reflects p2pg_drop_relays.  Writes
+ * min(cap, count) records, *n_out = count.  P2PG_ERR_STATE after a p2pg_update_edges at this
+ * round boundary or when the frontier (flood: and the one before it) was not kept.          */
+int p2pg_get_sends(p2pg_engine* e, int64_t cap, int32_t* sender, int32_t* receiver, int32_t* msg,
+                   uint8_t* lost, int64_t* n_out);
+/* The app did not relay these first receipts of the most recent round (its node_message made no
+ * send_to_nodes / send_to_node call for them, README.md:20): withdraw their sends before the
+ * next round -- flood, their frontier bits; gossip, the round's pushes are redone without them.
+ * Relay counters and the next round's `received` drop accordingly.  Each (peer[i], msg[i]) must
+ * be a first receipt of that round, listed once (P2PG_ERR_ARG otherwise, nothing changed).
+ * Read the round's deliveries first (they are its frontier bits).  Not on a vertex-partitioned
+ * rank, not after a p2pg_update_edges at this boundary.                                      */
+int p2pg_drop_relays(p2pg_engine* e, int64_t n, const int32_t* peer, const int32_t* msg);
 /* Validation copies: seen [V][W] uint64 (W = ceil(M/64)); hop/parent [V][M] int32 need
  * P2PG_FLAG_RECORD (-1 = not delivered).  Any pointer may be NULL.                      */
 int p2pg_read_planes(p2pg_engine* e, uint64_t* seen, int32_t* hop, int32_t* parent);

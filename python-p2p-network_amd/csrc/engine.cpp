@@ -180,6 +180,13 @@ struct p2pg_engine {
   hipStream_t side = nullptr;
   hipEvent_t ev_spare = nullptr, ev_main = nullptr;
   SeedStats seed;               // round 0's counters (seed_stats), valid for these sources / rows
+  // the arrivals of the next round (p2pg_round_stats.received): the last round's sends
+  // (send_to_node calls, less the relays p2pg_drop_relays withdrew) and how many of them are
+  // lost -- to churn (counted after every round of a churn run: cnt_lost) or to a connection a
+  // topology update removed (counted by p2pg_update_edges)
+  uint64_t sent_last = 0, lost_last = 0;
+  unsigned long long* d_cnt2 = nullptr;  // k_sends counters [2] (device) / pinned copy
+  unsigned long long* h_cnt2 = nullptr;
 };
 
 namespace {
@@ -208,6 +215,9 @@ void dfree(T*& p) {
 }
 
 void free_state(p2pg_engine* e) {
+  dfree(e->d_cnt2);
+  if (e->h_cnt2) (void)hipHostFree(e->h_cnt2);
+  e->h_cnt2 = nullptr;
   DevState& s = e->st;
   dfree(s.seen);
   if (e->seen_spare) {
@@ -544,6 +554,23 @@ int check_scatter_list(p2pg_engine* e, unsigned long long listed) {
   return P2PG_OK;
 }
 
+// Arrivals (p2pg_round_stats.received): a churn run counts the lost sends of every round.
+bool count_lost_on(const p2pg_engine* e) { return e->cfg.churn_threshold != 0; }
+
+// Enqueue the count of round r's lost sends (k_sends, count mode) over gs (the graph the sends
+// leave on; gone slots = removed connections) and gp (the graph round r's arrivals travelled
+// on: the senders' own first receipts); the count lands in h_cnt2[1] at the next stream sync.
+hipError_t enqueue_lost_count(p2pg_engine* e, const DevGraph& gs, const DevGraph& gp, int32_t r) {
+  hipError_t x = hipMemsetAsync(e->d_cnt2, 0, 2 * sizeof(unsigned long long), e->stream);
+  RoundParams p = params(e);
+  p.round = r;
+  if (x == hipSuccess)
+    x = launch_sends(gs, gp, e->st, p, false, 0, nullptr, nullptr, nullptr, nullptr, e->d_cnt2, e->stream);
+  if (x == hipSuccess)
+    x = hipMemcpyAsync(e->h_cnt2, e->d_cnt2, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, e->stream);
+  return x;
+}
+
 // Dense-round edge-mask planes E, sized by the current nnz: one, or two for fused rounds
 // (round r pulls E[(r-1)&1], pushes E[r&1]); only if they fit with headroom -- else gossip
 // pushes by row atomics only.  Replaces any previous planes (their contents are dropped).
@@ -621,6 +648,8 @@ int alloc_state(p2pg_engine* e) {
     if ((rc = A((void**)&s.parent, hb))) return rc;
   }
   if ((rc = A((void**)&s.stats, STAT_BYTES))) return rc;
+  if ((rc = A((void**)&e->d_cnt2, 2 * sizeof(unsigned long long)))) return rc;
+  HIPCHK(e, hipHostMalloc((void**)&e->h_cnt2, 2 * sizeof(unsigned long long)));
 #ifdef P2PG_PROF
   if ((rc = A((void**)&s.prof, sizeof(unsigned long long) * 16))) return rc;
   HIPCHK(e, hipMemset(s.prof, 0, sizeof(unsigned long long) * 16));
@@ -977,6 +1006,7 @@ int p2pg_reset(p2pg_engine* e) {
   e->last_push_e = false;
   e->consume_next = false;
   e->total_relays = 0;
+  e->sent_last = e->lost_last = 0;
   free_arr(e);
   e->prev_aw = e->prev_av = 0;
   e->last_new = 0;
@@ -1210,6 +1240,11 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
     if (r != hipSuccess) return fail(e, P2PG_ERR_HIP, std::string("step (exchange pack): ") + hipGetErrorString(r));
     e->auto_round = e->round;
   }
+  const bool cnt_lost = count_lost_on(e);
+  if (cnt_lost) {  // this round's lost sends: the next round's arrivals are its sends minus them
+    hipError_t x = enqueue_lost_count(e, g, graph_for_arrivals(e, e->round), e->round);
+    if (x != hipSuccess) return fail(e, P2PG_ERR_HIP, std::string("step (lost sends): ") + hipGetErrorString(x));
+  }
   if ((rc = read_stats())) return rc;
   std::memcpy(e->stats_base, e->h_stats, sizeof(e->stats_base));  // the next round counts from here
   if ((rc = check_scatter_list(e, e->h_stats[STAT_COUNT]))) return rc;
@@ -1244,7 +1279,11 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
                      : fused_round ? P2PG_PUSH_FUSED
                      : up_round ? P2PG_PUSH_UPDATE_EDGE
                      : e->last_push_e ? P2PG_PUSH_EDGE : P2PG_PUSH_ATOMIC;
+    out->reserved_ = 0;
+    out->received = e->round == 0 ? 0 : e->sent_last - e->lost_last;
   }
+  e->sent_last = tot[ST_RELAYS];
+  e->lost_last = cnt_lost ? (uint64_t)e->h_cnt2[1] : 0;
   e->total_relays += tot[ST_RELAYS];
   e->prev2_aw = e->prev_aw;
   e->prev2_av = e->prev_av;
@@ -1277,7 +1316,7 @@ constexpr int BATCH_MAX = 8;
 
 static bool decay_batchable(const p2pg_engine* e) {
   const int br = e->batch_rounds < 0 ? BATCH_MAX : e->batch_rounds;
-  return br > 1 && e->have_state && !e->done && !e->begun && e->round > 0 &&
+  return br > 1 && e->have_state && !e->done && !e->begun && e->round > 0 && !count_lost_on(e) &&
          e->cfg.mode == P2PG_MODE_GOSSIP && e->saw_dense && !e->last_push_e &&
          e->last_new < e->prev2_new && e->prev_sw > 0 && !e->consume_next && e->arr_round < 0 &&
          !e->d_gid && !(e->cfg.flags & P2PG_FLAG_NO_AUTOSTOP) && e->push_mode != 2 &&
@@ -1354,6 +1393,9 @@ static int run_decay_batch(p2pg_engine* e, int32_t R, p2pg_round_stats* out, int
     o.touched_words = tot[ST_AUX];
     o.push_form = P2PG_PUSH_ATOMIC;
     o.reserved_ = 0;
+    o.received = e->round == 0 ? 0 : e->sent_last - e->lost_last;
+    e->sent_last = tot[ST_RELAYS];
+    e->lost_last = 0;  // (no churn in a batched run)
     e->total_relays += tot[ST_RELAYS];
     e->frontier_kept_prev = e->frontier_kept;
     e->frontier_kept = !(partial[i] && active);
@@ -1400,7 +1442,7 @@ int p2pg_run(p2pg_engine* e, int32_t max_rounds, p2pg_round_stats* per_round,
     // only the last two rounds a call may run can leave frontiers behind for the caller (the
     // deliveries of the last round and their parents in the round before; snapshots); a
     // quiescent round has none
-    e->skip_frontier = n + 2 < max_rounds;
+    e->skip_frontier = n + 2 < max_rounds && !count_lost_on(e);  // (the lost count reads F)
     rc = p2pg_step(e, per_round ? &per_round[n] : &tmp);
     e->skip_frontier = false;
     if (rc < 0) return rc;
@@ -1471,6 +1513,161 @@ int p2pg_get_new_deliveries(p2pg_engine* e, int64_t cap, int32_t* peer, int32_t*
     parent[i] = (map && pr >= 0) ? e->h_gid[pr] : pr;
   }
   *n_out = (int64_t)cnt;
+  return P2PG_OK;
+}
+
+// Shared preconditions of the sends stream / relay withdrawal: a round ran, its frontier (and,
+// flood, the one before it: the senders' parents) is in F, and no topology update or half
+// round stands between that round and now.
+static int sends_state(p2pg_engine* e, const char* what) {
+  const std::string w(what);
+  if (!e->have_state || e->round == 0) return fail(e, P2PG_ERR_STATE, w + ": no round has run");
+  if (e->begun) return fail(e, P2PG_ERR_STATE, w + ": a round has begun (step_begin)");
+  if (e->arr_round >= 0 && e->arr_round == e->round)
+    return fail(e, P2PG_ERR_STATE, w + ": the connections changed since the round (call it before p2pg_update_edges)");
+  if (e->last_new == 0) return P2PG_OK;
+  if (!e->frontier_kept) return fail(e, P2PG_ERR_STATE, w + ": the last round's frontier was not kept");
+  if (e->cfg.mode == P2PG_MODE_FLOOD && e->round > 1 && !e->frontier_kept_prev)
+    return fail(e, P2PG_ERR_STATE, w + ": the senders' parents need the frontier of the round before, "
+                                       "which was not kept");
+  return P2PG_OK;
+}
+
+int p2pg_get_sends(p2pg_engine* e, int64_t cap, int32_t* sender, int32_t* receiver, int32_t* msg,
+                   uint8_t* lost, int64_t* n_out) {
+  if (!e || cap < 0 || !n_out || (cap > 0 && (!sender || !receiver || !msg || !lost)))
+    return fail(e, P2PG_ERR_ARG, "get_sends: bad arguments");
+  int rc = sends_state(e, "get_sends");
+  if (rc) return rc;
+  if (e->last_new == 0) {
+    *n_out = 0;
+    return P2PG_OK;
+  }
+  HIPCHK(e, hipSetDevice(e->cfg.device));
+  const int32_t r = e->round - 1;
+  RoundParams p = params(e);
+  p.round = r;
+  const int64_t c = cap > 0 ? cap : 1;
+  int32_t *ds = nullptr, *dr = nullptr, *dm = nullptr;
+  uint8_t* dl = nullptr;
+  HIPCHK(e, hipMalloc((void**)&ds, sizeof(int32_t) * c));
+  HIPCHK(e, hipMalloc((void**)&dr, sizeof(int32_t) * c));
+  HIPCHK(e, hipMalloc((void**)&dm, sizeof(int32_t) * c));
+  HIPCHK(e, hipMalloc((void**)&dl, c));
+  hipError_t lr = hipMemsetAsync(e->d_cnt2, 0, 2 * sizeof(unsigned long long), e->stream);
+  if (lr == hipSuccess)
+    lr = launch_sends(graph(e), graph_for_arrivals(e, r), e->st, p, true, cap, ds, dr, dm, dl, e->d_cnt2, e->stream);
+  unsigned long long cnt = 0;
+  if (lr == hipSuccess) lr = hipMemcpyAsync(&cnt, e->d_cnt2, sizeof(cnt), hipMemcpyDeviceToHost, e->stream);
+  if (lr == hipSuccess) lr = hipStreamSynchronize(e->stream);
+  const int64_t n = std::min<int64_t>((int64_t)cnt, cap);
+  std::vector<int32_t> hs(n), hr(n), hm(n);
+  std::vector<uint8_t> hl(n);
+  if (lr == hipSuccess && n > 0) {
+    lr = hipMemcpy(hs.data(), ds, sizeof(int32_t) * n, hipMemcpyDeviceToHost);
+    if (lr == hipSuccess) lr = hipMemcpy(hr.data(), dr, sizeof(int32_t) * n, hipMemcpyDeviceToHost);
+    if (lr == hipSuccess) lr = hipMemcpy(hm.data(), dm, sizeof(int32_t) * n, hipMemcpyDeviceToHost);
+    if (lr == hipSuccess) lr = hipMemcpy(hl.data(), dl, n, hipMemcpyDeviceToHost);
+  }
+  (void)hipFree(ds);
+  (void)hipFree(dr);
+  (void)hipFree(dm);
+  (void)hipFree(dl);
+  if (lr != hipSuccess) return fail(e, P2PG_ERR_HIP, std::string("get_sends: ") + hipGetErrorString(lr));
+  // deterministic order: ascending (receiver, sender, msg) -- the harness's delivery order up to the
+  // order of one sender's packets on one connection, which the caller knows (its relay order)
+  std::vector<int64_t> idx(n);
+  std::iota(idx.begin(), idx.end(), 0);
+  std::sort(idx.begin(), idx.end(), [&](int64_t a, int64_t b) {
+    if (hr[a] != hr[b]) return hr[a] < hr[b];
+    return hs[a] != hs[b] ? hs[a] < hs[b] : hm[a] < hm[b];
+  });
+  const bool map = !e->h_gid.empty();
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t k = idx[i];
+    sender[i] = map ? e->h_gid[hs[k]] : hs[k];
+    receiver[i] = map ? e->h_gid[hr[k]] : hr[k];
+    msg[i] = hm[k];
+    lost[i] = hl[k];
+  }
+  *n_out = (int64_t)cnt;
+  return P2PG_OK;
+}
+
+int p2pg_drop_relays(p2pg_engine* e, int64_t n, const int32_t* peer, const int32_t* msg) {
+  if (!e || n < 0 || (n > 0 && (!peer || !msg))) return fail(e, P2PG_ERR_ARG, "drop_relays: bad arguments");
+  int rc = sends_state(e, "drop_relays");
+  if (rc) return rc;
+  if (n == 0) return P2PG_OK;
+  if (e->d_gid || (e->cfg.flags & P2PG_FLAG_LOCAL_GRAPH))
+    return fail(e, P2PG_ERR_STATE, "drop_relays: not on a vertex-partitioned rank");
+  const bool gossip = e->cfg.mode == P2PG_MODE_GOSSIP;
+  if (!gossip && e->consume_next)
+    return fail(e, P2PG_ERR_STATE, "drop_relays: the last round's sends were materialized (restored snapshot)");
+  std::vector<uint64_t> list(n);
+  for (int64_t i = 0; i < n; ++i) {
+    if (peer[i] < 0 || peer[i] >= e->V || msg[i] < 0 || msg[i] >= e->M)
+      return fail(e, P2PG_ERR_ARG, "drop_relays: peer or message out of range");
+    list[i] = ((uint64_t)(uint32_t)peer[i] << 32) | (uint32_t)msg[i];
+  }
+  std::sort(list.begin(), list.end());
+  if (std::adjacent_find(list.begin(), list.end()) != list.end())
+    return fail(e, P2PG_ERR_ARG, "drop_relays: a first receipt is listed twice");
+  HIPCHK(e, hipSetDevice(e->cfg.device));
+  const int32_t r = e->round - 1;
+  uint64_t* dl = nullptr;
+  HIPCHK(e, hipMalloc((void**)&dl, sizeof(uint64_t) * n));
+  hipError_t lr = hipMemcpyAsync(dl, list.data(), sizeof(uint64_t) * n, hipMemcpyHostToDevice, e->stream);
+  if (lr == hipSuccess) lr = hipMemsetAsync(e->d_cnt2, 0, 2 * sizeof(unsigned long long), e->stream);
+  if (lr == hipSuccess) lr = launch_drop(e->st, r, dl, n, true, e->d_cnt2, e->stream);
+  if (lr == hipSuccess)
+    lr = hipMemcpyAsync(e->h_cnt2, e->d_cnt2, sizeof(unsigned long long), hipMemcpyDeviceToHost, e->stream);
+  if (lr == hipSuccess) lr = hipStreamSynchronize(e->stream);
+  if (lr == hipSuccess && (int64_t)e->h_cnt2[0] != n) {
+    (void)hipFree(dl);
+    return fail(e, P2PG_ERR_ARG, "drop_relays: " + std::to_string(n - (int64_t)e->h_cnt2[0]) +
+                                     " listed (peer, msg) are not first receipts of the last round");
+  }
+  if (lr == hipSuccess) lr = launch_drop(e->st, r, dl, n, false, nullptr, e->stream);
+  if (lr == hipSuccess) lr = launch_rebuild_aw(e->st, r, e->V, e->stream);
+  // the relays these receipts would have made (node.py:106-116): flood every connection but
+  // the sender (all of them at the origin), gossip min(k, deg)
+  uint64_t cancelled = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t v = (int64_t)(list[i] >> 32);
+    const uint64_t deg = (uint64_t)(e->h_rowptr[v + 1] - e->h_rowptr[v]);
+    cancelled += gossip ? std::min<uint64_t>(deg, (uint64_t)e->cfg.fanout) : (r == 0 ? deg : (deg ? deg - 1 : 0));
+  }
+  if (lr == hipSuccess && gossip) {
+    // this round's pushes left inside the round: push the remaining receipts again, as row
+    // atomics, into the cleared row-push planes the next round consumes (the Philox picks are a
+    // pure function of round, peer and message, so the others go where they went)
+    DevState& s = e->st;
+    const int nx = e->round & 1;
+    lr = hipMemsetAsync(s.next[nx], 0, e->plane_bytes, e->stream);
+    if (lr == hipSuccess) lr = hipMemsetAsync(s.T[nx], 0, e->bm_bytes, e->stream);
+    RoundParams p = params(e);
+    p.round = r;
+    if (lr == hipSuccess) lr = launch_scatter_atomic(e, graph(e), p, std::max<uint64_t>(e->prev_aw, 1));
+  }
+  if (lr == hipSuccess && count_lost_on(e))
+    lr = enqueue_lost_count(e, graph(e), graph_for_arrivals(e, r), r);
+  if (lr == hipSuccess) lr = hipStreamSynchronize(e->stream);
+  (void)hipFree(dl);
+  if (lr != hipSuccess) return fail(e, P2PG_ERR_HIP, std::string("drop_relays: ") + hipGetErrorString(lr));
+  if (gossip) {
+    if (e->wlist_check) {
+      unsigned long long listed = 0;
+      HIPCHK(e, hipMemcpy(&listed, e->st.stats + STAT_COUNT, sizeof(listed), hipMemcpyDeviceToHost));
+      if ((rc = check_scatter_list(e, listed))) return rc;
+    }
+    e->consume_next = true;
+    e->last_push_e = false;
+    e->stats_clear = true;  // the re-push counted into the round counters
+  }
+  if (count_lost_on(e)) e->lost_last = (uint64_t)e->h_cnt2[1];
+  e->sent_last -= std::min(cancelled, e->sent_last);
+  e->total_relays -= std::min(cancelled, e->total_relays);
   return P2PG_OK;
 }
 
@@ -1788,11 +1985,27 @@ int p2pg_update_edges(p2pg_engine* e, int64_t n_add, const int32_t* add, int64_t
     // next[round&1] over the old graph minus the removed slots, before the graph changes.
     DevState& s = e->st;
     const bool gossip = e->cfg.mode == P2PG_MODE_GOSSIP;
-    free_arr(e);
     std::vector<uint8_t> gone(ci.size(), 0);
     for (const auto& d : dels) gone[slot_of(d.first, d.second)] = 1;
-    HIPCHK(e, hipMalloc((void**)&e->d_gone, gone.empty() ? 1 : gone.size()));
-    if (!gone.empty()) HIPCHK(e, hipMemcpy(e->d_gone, gone.data(), gone.size(), hipMemcpyHostToDevice));
+    uint8_t* d_gone = nullptr;
+    HIPCHK(e, hipMalloc((void**)&d_gone, gone.empty() ? 1 : gone.size()));
+    if (!gone.empty()) HIPCHK(e, hipMemcpy(d_gone, gone.data(), gone.size(), hipMemcpyHostToDevice));
+    if (!dels.empty()) {
+      // the arrivals of the next round lose the sends in flight on the removed connections: count
+      // the last round's lost sends again with those slots gone (churn losses included), while the
+      // graph its own arrivals travelled on (the senders' first receipts) is still at hand
+      DevGraph gs = graph(e);
+      gs.gone = d_gone;
+      hipError_t x = enqueue_lost_count(e, gs, graph_for_arrivals(e, e->round - 1), e->round - 1);
+      if (x == hipSuccess) x = hipStreamSynchronize(e->stream);
+      if (x != hipSuccess) {
+        (void)hipFree(d_gone);
+        return fail(e, P2PG_ERR_HIP, std::string("update_edges (lost sends): ") + hipGetErrorString(x));
+      }
+      e->lost_last = (uint64_t)e->h_cnt2[1];
+    }
+    free_arr(e);
+    e->d_gone = d_gone;
     if (!s.next[0]) {  // flood: row-push planes on first use
       for (int i = 0; i < 2; ++i) {
         HIPCHK(e, hipMalloc((void**)&s.next[i], e->plane_bytes ? e->plane_bytes : 8));
@@ -1848,7 +2061,7 @@ int p2pg_update_edges(p2pg_engine* e, int64_t n_add, const int32_t* add, int64_t
 namespace {
 
 constexpr uint64_t SNAP_MAGIC = 0x50414E5347503250ull;  // "P2PGSNAP"
-constexpr uint32_t SNAP_VERSION = 2;  // 2: + last_new
+constexpr uint32_t SNAP_VERSION = 3;  // 2: + last_new; 3: + sent_last / lost_last
 
 struct SnapHeader {
   uint64_t magic;
@@ -1859,6 +2072,7 @@ struct SnapHeader {
   uint32_t consume_next, has_next;
   uint64_t gossip_seed, churn_seed, graph_hash, src_hash, total_relays, prev_aw, prev_av;
   uint64_t last_new;  // first receipts of the last round (deliveries, decay-phase push dedup)
+  uint64_t sent_last, lost_last;  // the next round's arrivals (p2pg_round_stats.received)
 };
 
 uint64_t fnv1a(uint64_t h, const void* data, size_t n) {
@@ -1970,6 +2184,8 @@ int p2pg_snapshot(p2pg_engine* e, void* buf, int64_t cap) {
   h.prev_aw = e->prev_aw;
   h.prev_av = e->prev_av;
   h.last_new = e->last_new;
+  h.sent_last = e->sent_last;
+  h.lost_last = e->lost_last;
   char* out = (char*)buf;
   std::memcpy(out, &h, sizeof(h));
   size_t off = sizeof(h);
@@ -2029,6 +2245,8 @@ int p2pg_restore(p2pg_engine* e, const void* buf, int64_t size) {
   e->prev_aw = h.prev_aw;
   e->prev_av = h.prev_av;
   e->last_new = h.last_new;
+  e->sent_last = h.sent_last;
+  e->lost_last = h.lost_last;
   // the snapshot holds the last round's frontier, not the one before it, so that round's
   // delivery parents cannot be found (round 0's are -1): deliveries refuse it, as documented
   e->frontier_kept = true;
@@ -2043,6 +2261,13 @@ int p2pg_restore(p2pg_engine* e, const void* buf, int64_t size) {
   });
   if (rc) return rc;
   HIPCHK(e, hipMemsetAsync(s.A[e->round & 1], 0, e->bm_bytes, e->stream));
+  // the last round's active-word masks are not in the snapshot: rebuilt from its frontier rows
+  // (a re-push after a topology update, and the next sparse push, list words by them)
+  if (e->round > 0) {
+    hipError_t x = launch_rebuild_aw(s, e->round - 1, e->V, e->stream);
+    if (x == hipSuccess) x = hipStreamSynchronize(e->stream);
+    if (x != hipSuccess) return fail(e, P2PG_ERR_HIP, std::string("restore: ") + hipGetErrorString(x));
+  }
   return P2PG_OK;
 }
 

@@ -61,6 +61,7 @@ class RoundStatsC(ctypes.Structure):
         ("touched_words", ctypes.c_uint64),
         ("push_form", ctypes.c_int32),
         ("reserved_", ctypes.c_int32),
+        ("received", ctypes.c_uint64),
     ]
 
 
@@ -88,6 +89,8 @@ SIGNATURES = {
     "p2pg_step": (ctypes.c_int, [_P, ctypes.POINTER(RoundStatsC)]),
     "p2pg_run": (ctypes.c_int, [_P, _I32, _P, ctypes.POINTER(_I32)]),
     "p2pg_get_new_deliveries": (ctypes.c_int, [_P, _I64, _P, _P, _P, _P, ctypes.POINTER(_I64)]),
+    "p2pg_get_sends": (ctypes.c_int, [_P, _I64, _P, _P, _P, _P, ctypes.POINTER(_I64)]),
+    "p2pg_drop_relays": (ctypes.c_int, [_P, _I64, _P, _P]),
     "p2pg_read_planes": (ctypes.c_int, [_P, _P, _P, _P]),
     "p2pg_read_seen_word": (ctypes.c_int, [_P, _I32, _P]),
     "p2pg_kernel_times": (ctypes.c_int, [_P, _P, _P]),

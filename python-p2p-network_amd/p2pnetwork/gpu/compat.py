@@ -1,19 +1,41 @@
 """Per-callback compatibility mode: ``Node``-subclass apps on a simulated peer graph.
 
-``CompatNetwork`` builds one app object per peer of a ``PeerGraph`` and drives them from the
-HIP engine: every round's first receipts are handed to the receiving peer's
-``node_message(connection, data)``, in a fixed order (ascending peer, then message), on the
-calling thread.  One Python call per delivery, so this is for small graphs; the batched hook of
-``GraphNetwork`` is the fast path.
+``CompatNetwork`` builds one app object per peer of a ``PeerGraph`` and runs them round-
+synchronously with the reference's hook semantics: every packet that arrives is counted
+(``message_count_recv``) and handed to the receiver's ``node_message(connection, data)``
+(NodeConnection.run, p2pnetwork/nodeconnection.py:211-216), duplicates included, and the app
+alone decides what to send (README.md:20).  One Python call per arrival, so this is for small
+graphs; the batched hook of ``GraphNetwork`` is the fast path.
 
-What an app sees is the *contract* of the reference's hook surface, not
-its implementation:
+Who carries the packets:
+
+* The HIP engine carries every *relay it can express*: a broadcast originated with
+  ``send_to_nodes(data)`` (node.py:106-112) becomes an engine message, and a first receipt of it
+  that the app forwards the way the engine would -- flood: ``send_to_nodes(data, exclude=[the
+  sender])``, or ``send_to_node`` on exactly those connections; gossip (build-defined, SURVEY.md
+  A.3): ``send_to_nodes(data, ...)``, or ``send_to_node`` on exactly the k Philox picks -- stays
+  in the engine's frontier.  A first receipt the app does not forward is withdrawn
+  (``p2pg_drop_relays``).  The engine's sends of each round (``p2pg_get_sends``: every
+  ``send_to_node`` call, the ones churn loses flagged) are the next round's arrivals.
+* Every other send -- a different payload, a different target set, a second relay of the same
+  message, a duplicate's relay, ``NodeConnection.send`` -- is carried by the host as an explicit
+  packet, subject to the same churn rule.  For the dedup-relay apps of the reference's
+  documentation and fixtures this path stays empty (``explicit_packets`` counts it).
+
+Delivery order inside a round is the reference harness's: ascending receiver, then sender, then
+the order the sender wrote the packets (its own hook order of the round before).  A connection's
+byte stream is framed like NodeConnection.run, with its quirks: a body holding 0x04 arrives as
+several packets, an empty packet (EOT at position 0) stops the stream for good
+(nodeconnection.py:211).
+
+What an app sees is the *contract* of the reference's hook surface:
 
 * the hook names and the ``callback(event, main_node, connected_node, data)`` signature of
-  p2pnetwork/node.py:25-29 (every hook fires the callback with the reference's argument shape);
+  node.py:25-29 (every hook fires the callback with the reference's argument shape);
 * ``nodes_inbound`` / ``nodes_outbound`` / ``all_nodes`` (node.py:75-78), the message counters
-  (node.py:65-67), ``send_to_nodes`` / ``send_to_node`` (node.py:106-120) and
-  ``connect_with_node`` / ``disconnect_with_node`` (node.py:122-189);
+  (node.py:65-67: send += 1 per ``send_to_node`` call before anything else, :116; recv += 1 per
+  delivered packet, nodeconnection.py:215), ``send_to_nodes`` / ``send_to_node`` (node.py:106-120)
+  and ``connect_with_node`` / ``disconnect_with_node`` (node.py:122-189);
 * connection handles with ``id`` / ``host`` / ``port``, ``send``, ``set_info`` / ``get_info``.
 
 Out of scope: sockets and threads, sha512 ids (a peer's id is its engine
@@ -28,33 +50,25 @@ Port an app by swapping its base class::
             ...
 
     net = CompatNetwork(graph, MyNode)
-    net.nodes[0].send_to_nodes({"mid": 1})    # originates a broadcast
+    net.nodes[0].send_to_nodes({"mid": 1})    # queued; sent when run() starts (round 0)
     net.run()
 
-Semantics:
+Semantics beyond the hooks:
 
 * Connections: for every edge {a, b} with a < b, a dialled b (a's ``nodes_outbound`` holds the
   handle to b, b's ``nodes_inbound`` the handle to a); both connected events fire per edge,
   ascending (a, b), at construction.
-* Origination: ``send_to_nodes(data)`` outside a delivery queues a broadcast; ``run()`` relays
-  the broadcasts queued since the previous ``run()`` (engine message ids count from 0 per run).
-  Receivers get ``data`` after the wire codec (``wire.round_trip``: tuples arrive as lists, a str
-  holding JSON arrives parsed); an unsendable payload reaches nobody (nodeconnection.py:158-160).
-* Relay: the engine performs the dedup relay (flood: every connection but the sender; gossip:
-  k Philox-chosen connections).  ``send_to_nodes`` / ``send_to_node`` made *inside*
-  ``node_message`` are the app's relay of the message being delivered; they are absorbed
-  (``CompatNetwork.absorbed_sends``), never sent twice.
-* Counters: ``message_count_send`` = relays the engine made for the peer (every attempted send,
-  also those churn drops, node.py:116); ``message_count_recv`` = its first receipts.
+* ``run()`` sends what was queued since the previous ``run()`` in round 0 and runs rounds until
+  nothing is in flight; rounds (``current_round``) and engine message ids count from 0 per run.
 * Connection changes (also from inside ``node_message``) take effect between rounds through the
-  engine's ``update_edges``: a removed connection loses the messages in flight on it and both
-  ends see ``node_disconnected``; a new one fires the connected events when it appears.
+  engine's ``update_edges``: a removed connection loses the packets in flight on it and both ends
+  see ``node_disconnected``; a new one fires the connected events when it appears.
 """
 import threading
 
 import numpy as np
 
-from . import wire
+from . import _lib, wire
 
 # Lifecycle hooks and the shape of the callback they fire (node.py:282-352):
 #   "conn"  -> callback(event, self, connection, {})
@@ -98,7 +112,8 @@ class SimConnection:
         self.terminate_flag = threading.Event()
 
     def send(self, data, encoding_type="utf-8", compression="none"):
-        self.main_node._net._single_send(self.main_node, self, data, compression)
+        """NodeConnection.send (nodeconnection.py:107-160): one packet, no counter."""
+        self.main_node._net._raw_send(self.main_node, self, data, encoding_type, compression)
 
     def parse_packet(self, packet):
         return wire.parse_packet(packet)
@@ -170,7 +185,7 @@ class SimNode:
         return True
 
     def disconnect_with_node(self, node):
-        """Close one of our outbound connections; it goes away between rounds (messages in
+        """Close one of our outbound connections; it goes away between rounds (packets in
         flight on it are lost) and both ends then see node_disconnected."""
         if node not in self.nodes_outbound:
             return
@@ -197,13 +212,21 @@ for _event, _shape in _HOOK_SHAPES.items():
 del _event, _shape
 
 
+def _single_frame(pkt):
+    """True if the receiver's framing yields exactly this one packet (no 0x04 inside the body,
+    body not empty): only such payloads can be engine messages."""
+    return len(pkt) > 1 and pkt.find(wire.EOT_CHAR) == len(pkt) - 1
+
+
 class CompatNetwork:
     """A population of ``node_class`` instances over ``graph``, relayed by the HIP engine."""
 
     def __init__(self, graph, node_class=SimNode, mode="flood", fanout=3, host="127.0.0.1",
-                 base_port=10000, node_kwargs=None, engine_factory=None, **engine_kw):
+                 base_port=10000, node_kwargs=None, engine_factory=None, gossip_seed=0x5EED,
+                 churn_threshold_value=0, churn_seed=0xC0FFEE, **engine_kw):
         from .network import GraphNetwork
         self.graph, self.mode, self.fanout = graph, mode, int(fanout)
+        self.gossip_seed, self.churn_thr, self.churn_seed = int(gossip_seed), int(churn_threshold_value), int(churn_seed)
         kw = dict(node_kwargs or {})
         self.nodes = []
         for v in range(graph.V):
@@ -217,12 +240,22 @@ class CompatNetwork:
         self._deg = graph.degree()
         self._pending = {}   # {(min, max): (connect?, dialler, other)} for the next round boundary
         make = engine_factory or GraphNetwork
-        self.engine = make(graph, mode=mode, fanout=fanout, **engine_kw)
-        self.origins, self.payloads = [], []
-        self._consumed = 0   # broadcasts relayed by earlier run() calls
-        self.absorbed_sends = 0
+        self.engine = make(graph, mode=mode, fanout=fanout, gossip_seed=gossip_seed,
+                           churn_threshold_value=churn_threshold_value, churn_seed=churn_seed,
+                           **engine_kw)
         self.current_round = -1
-        self._in_delivery = False
+        self.canonical_relays = 0   # first receipts relayed by the engine (its frontier)
+        self.explicit_packets = 0   # packets the host carried (sends the engine cannot express)
+        self._seq = 0
+        self._q_orig = []           # queued originations: (peer, packet, seq)
+        self._q_explicit = []       # queued explicit packets: (sender, receiver, seq, packet)
+        self._streams = {}          # (sender, receiver) -> bytes not yet framed
+        self._wedged = set()        # (sender, receiver) streams stopped by an empty packet
+        self._ctx = None            # (receiver, sender, engine msg or None) during node_message
+        self._first = {}            # engine first receipts of the round: (peer, msg) -> parent
+        self._claims = {}           # (peer, msg) -> ("nodes", seq) | ("node", {target: seq})
+        self._packets = []          # engine message -> its packet bytes
+        self._engine_live = False   # the engine runs this run()'s broadcasts
 
     # -- wiring -------------------------------------------------------------------------------
     def _link_all(self, pairs):
@@ -256,91 +289,251 @@ class CompatNetwork:
         else:
             self._pending[key] = (connect, a, b)
 
-    def _apply_changes(self):
+    def _apply_changes(self, in_flight=None):
         """Hand the queued changes to the engine (p2pg_update_edges), then mirror them on the
         node objects: removed handles + node_disconnected on both ends, new handles + the
-        connected events (dialler outbound, other end inbound)."""
+        connected events (dialler outbound, other end inbound).  Packets in flight on a removed
+        connection are lost (its reader stopped, nodeconnection.py:192-228)."""
         if not self._pending:
-            return
+            return in_flight
         changes, self._pending = self._pending, {}
         add = [(a, b) for _, (c, a, b) in sorted(changes.items()) if c]  # (dialler, other)
         rem = sorted(k for k, (c, _, _) in changes.items() if not c)
         self.engine.update_edges(add=add, remove=rem)
         self.graph = self.engine.graph
         self._deg = self.graph.degree()
+        gone = set()
         for a, b in rem:
+            gone |= {(a, b), (b, a)}
             ca, cb = self._links[a].pop(b), self._links[b].pop(a)
             self.nodes[a].node_disconnected(ca)
             self.nodes[b].node_disconnected(cb)
+            for k in ((a, b), (b, a)):
+                self._streams.pop(k, None)
+                self._wedged.discard(k)
         self._link_all(add)
+        if in_flight is not None and gone:
+            in_flight = [x for x in in_flight if (x[1], x[0]) not in gone]
+        return in_flight
 
     # -- sends from app code --------------------------------------------------------------------
+    def _next_seq(self):
+        self._seq += 1
+        return self._seq
+
+    def _engine_msg_of(self, node, pkt):
+        """The engine message this send may relay: the one being delivered to `node`, if the
+        packet is that message's and `node` got it first this round (a first receipt)."""
+        ctx = self._ctx
+        if ctx is None or ctx[0] != node._peer or ctx[2] is None:
+            return None
+        m = ctx[2]
+        if (node._peer, m) not in self._first or pkt != self._packets[m]:
+            return None
+        return m
+
+    def _explicit(self, v, targets, seq, pkt):
+        for u in targets:
+            self._q_explicit.append((v, u, seq, pkt))
+        self.explicit_packets += len(targets)
+
     def _broadcast_send(self, node, data, exclude, compression):
-        if self._in_delivery:
-            self.absorbed_sends += 1  # the engine already relays the message being delivered
-            return
+        """Node.send_to_nodes (node.py:106-112): send_to_node on every connection not excluded
+        (identity filter), each counted before it is sent (:116)."""
         if node._net is not self:
             raise ValueError("node does not belong to this CompatNetwork")
-        if exclude:
-            raise NotImplementedError("compat mode: a broadcast originates to every connection")
-        ok, obj = wire.round_trip(data, compression=compression)
-        if ok:
-            self.origins.append(node._peer)
-            self.payloads.append(obj)
-        else:  # nothing reaches the wire, but every attempt is counted (node.py:116)
-            node.message_count_send += len(node.all_nodes)
+        targets = [c for c in node.all_nodes if c not in exclude]
+        pkt = wire.encode_packet(data, compression=compression)
+        seq = self._next_seq()
+        v = node._peer
+        gossip = self.mode == "gossip"
+        if self._ctx is None:
+            if pkt is not None and not exclude and _single_frame(pkt):
+                # a new broadcast: an engine message, originated in round 0 of the next run()
+                node.message_count_send += min(self.fanout, len(targets)) if gossip else len(targets)
+                self._q_orig.append((v, pkt, seq))
+                return
+            node.message_count_send += len(targets)
+            if pkt is not None:
+                self._explicit(v, [c.peer for c in targets], seq, pkt)
+            return
+        m = self._engine_msg_of(node, pkt) if pkt is not None else None
+        if m is not None and (v, m) not in self._claims:
+            deg = int(self._deg[v])
+            if gossip:  # the gossip relay: the engine's k picks (SURVEY.md A.3)
+                node.message_count_send += min(self.fanout, deg)
+                self._claims[(v, m)] = ("nodes", seq)
+                return
+            parent = self._first[(v, m)]
+            if len(targets) == deg - 1 and all(c.peer != parent for c in targets):
+                node.message_count_send += len(targets)
+                self._claims[(v, m)] = ("nodes", seq)
+                return
+        node.message_count_send += len(targets)
+        if pkt is not None:
+            self._explicit(v, [c.peer for c in targets], seq, pkt)
 
     def _single_send(self, node, conn, data, compression):
-        if self._in_delivery:
-            self.absorbed_sends += 1
+        """Node.send_to_node (node.py:114-120): counted first, sent only over a connection the
+        node still has."""
+        node.message_count_send += 1
+        if conn not in node.all_nodes:
             return
-        raise NotImplementedError("compat mode: a single-connection send outside a delivery is not a "
-                                  "broadcast; use send_to_nodes")
+        pkt = wire.encode_packet(data, compression=compression)
+        seq = self._next_seq()
+        if pkt is None:
+            return
+        v = node._peer
+        m = self._engine_msg_of(node, pkt)
+        if m is not None:
+            c = self._claims.get((v, m))
+            if c is None:
+                c = self._claims[(v, m)] = ("node", {})
+            if c[0] == "node" and conn.peer not in c[1]:
+                c[1][conn.peer] = seq
+                return
+        self._explicit(v, [conn.peer], seq, pkt)
+
+    def _raw_send(self, node, conn, data, encoding_type, compression):
+        """NodeConnection.send called by the app itself: one packet, no counter."""
+        pkt = wire.encode_packet(data, encoding_type, compression)
+        seq = self._next_seq()
+        if pkt is not None:
+            self._explicit(node._peer, [conn.peer], seq, pkt)
+
+    def gossip_connections(self, node, m):
+        """The connections the engine's gossip picks for a first receipt of engine message m at
+        `node` in the current round -- send_to_node on exactly these is relayed
+        by the engine."""
+        v = node._peer
+        nb = self.graph.neighbours(v)
+        out = np.zeros(max(self.fanout, 1), dtype=np.uint32)
+        n = _lib.check(_lib.lib().p2pg_gossip_targets(max(self.current_round, 0), v, int(m), len(nb),
+                                                      self.fanout, self.gossip_seed, _lib.ptr(out)))
+        return [self._links[v][int(nb[j])] for j in out[:n]]
 
     # -- running --------------------------------------------------------------------------------
-    def run(self, max_rounds=1 << 20):
-        """Relay the broadcasts queued since the last run to quiescence, dispatching hooks per
-        round; returns the engine's per-round stats."""
-        self._apply_changes()  # changes made before the run: its starting topology
-        base = self._consumed
-        if base == len(self.origins):
-            return []
-        self._consumed = len(self.origins)
-        self.engine.broadcast(np.asarray(self.origins[base:], dtype=np.int32))
+    def _lost(self, rnd, a, b):
+        return self.churn_thr != 0 and _lib.lib().p2pg_churn_lost(rnd, a, b, self.churn_thr, self.churn_seed) != 0
+
+    def _canonical(self, v, m, parent):
+        """The targets of the engine's relay of first receipt (v, m)."""
+        nb = self.graph.neighbours(v)
+        if self.mode == "flood":
+            return {int(u) for u in nb if u != parent}
+        return {c.peer for c in self.gossip_connections(self.nodes[v], m)}
+
+    def _resolve(self, rnd):
+        """After a round's hooks: first receipts the app relayed as the engine would stay in its
+        frontier (their sends get the seq of the app's call); the others are withdrawn, and their
+        partial relays travel as explicit packets."""
+        order, drop = {}, []
+        for (v, m), parent in self._first.items():
+            c = self._claims.get((v, m))
+            if c is not None and c[0] == "nodes":
+                order[(v, m)] = c[1]
+                continue
+            if c is not None and set(c[1]) == self._canonical(v, m, parent):
+                order[(v, m)] = c[1]
+                continue
+            drop.append((v, m))
+            if c is not None:
+                for u, seq in c[1].items():
+                    self._explicit(v, [u], seq, self._packets[m])
+        self.canonical_relays += len(order)
+        if drop:
+            d = np.asarray(drop, dtype=np.int32).reshape(-1, 2)
+            self.engine.drop_relays(d[:, 0], d[:, 1])
+        return order
+
+    def _in_flight(self, rnd, order):
+        """The packets of round rnd: the engine's sends (after withdrawals) and the explicit
+        ones, as (receiver, sender, seq, engine msg or None, packet, lost)."""
         out = []
-        while len(out) < max_rounds:
-            st = self.engine.step()
-            out.append(st)
-            self.current_round = st.round
-            if st.new_deliveries:
-                d = self.engine.deliveries()
-                for i in np.lexsort((d.msg, d.peer)):
-                    self._deliver(int(d.peer[i]), base + int(d.msg[i]), int(d.parent[i]), st.round)
-            self.between_rounds(st.round)
-            self._apply_changes()  # made by this round's hooks: effective from the next round
-            if not st.active:
-                break
+        if order:
+            s = self.engine.sends()
+            for a, b, m, lost in zip(s.sender.tolist(), s.receiver.tolist(), s.msg.tolist(), s.lost.tolist()):
+                o = order[(a, m)]
+                out.append((b, a, o if isinstance(o, int) else o[b], m, self._packets[m], lost))
+        for a, b, seq, pkt in self._q_explicit:
+            out.append((b, a, seq, None, pkt, self._lost(rnd, a, b)))
+        self._q_explicit = []
         return out
+
+    def _deliver(self, arrivals):
+        """NodeConnection.run for every connection, in the harness's order: bytes appended to
+        the stream, framed on 0x04 (nodeconnection.py:204-214), each packet counted and handed to
+        node_message (:215-216)."""
+        for rcv, snd, _, m, pkt, lost in sorted(arrivals, key=lambda x: (x[0], x[1], x[2])):
+            if lost:
+                continue
+            key = (snd, rcv)
+            if key in self._wedged:
+                continue
+            conn = self._links[rcv].get(snd)
+            if conn is None:
+                continue
+            buf = self._streams.pop(key, b"") + pkt
+            packets, rest = wire.split_stream(buf)
+            if rest:
+                if rest[:1] == wire.EOT_CHAR:
+                    self._wedged.add(key)  # eot_pos == 0: the loop never delivers again
+                else:
+                    self._streams[key] = rest
+            node = self.nodes[rcv]
+            one = len(packets) == 1 and not rest
+            for p in packets:
+                node.message_count_recv += 1
+                self._ctx = (rcv, snd, m if one else None)
+                try:
+                    node.node_message(conn, wire.parse_packet(p))
+                finally:
+                    self._ctx = None
+
+    def run(self, max_rounds=1 << 20):
+        """Send what was queued since the last run (round 0), then deliver and dispatch round by
+        round until nothing is in flight; returns the engine's per-round stats."""
+        self._engine_live = False
+        self._apply_changes()  # changes made before the run: its starting topology
+        if not self._q_orig and not self._q_explicit:
+            return []
+        orig, self._q_orig = self._q_orig, []
+        self._packets = [pkt for _, pkt, _ in orig]
+        stats = []
+        order = {}
+        self.current_round = 0
+        if orig:
+            self.engine.broadcast(np.asarray([v for v, _, _ in orig], dtype=np.int32))
+            self._engine_live = True
+            st = self.engine.step()
+            stats.append(st)
+            order = {(v, m): seq for m, (v, _, seq) in enumerate(orig)}
+            self.canonical_relays += len(orig)
+        arrivals = self._in_flight(0, order)
+        self.between_rounds(0)
+        arrivals = self._apply_changes(arrivals)
+        rnd = 0
+        while any(not x[5] for x in arrivals) and rnd < max_rounds:
+            rnd += 1
+            self.current_round = rnd
+            self._first, self._claims = {}, {}
+            if self._engine_live and stats and stats[-1].active:
+                st = self.engine.step()
+                stats.append(st)
+                if st.new_deliveries:
+                    d = self.engine.deliveries()
+                    self._first = dict(zip(zip(d.peer.tolist(), d.msg.tolist()), d.parent.tolist()))
+            self._deliver(arrivals)
+            order = self._resolve(rnd)
+            arrivals = self._in_flight(rnd, order)
+            self._first, self._claims = {}, {}
+            self.between_rounds(rnd)
+            arrivals = self._apply_changes(arrivals)
+        return stats
 
     def between_rounds(self, rnd):
         """Called after round rnd's node_message calls, before queued connection changes are
         applied (override to drive topology changes from outside the nodes)."""
-
-    def _deliver(self, v, payload_idx, parent, rnd):
-        node = self.nodes[v]
-        deg = int(self._deg[v])
-        if self.mode == "gossip":
-            node.message_count_send += min(self.fanout, deg)
-        else:
-            node.message_count_send += deg if rnd == 0 else max(deg - 1, 0)
-        if rnd == 0:
-            return  # the origin's own send_to_nodes; it gets no node_message
-        node.message_count_recv += 1
-        self._in_delivery = True
-        try:
-            node.node_message(self._links[v][parent], self.payloads[payload_idx])
-        finally:
-            self._in_delivery = False
 
     def close(self):
         self.engine.close()

@@ -30,7 +30,7 @@ from .graph import PeerGraph
 PUSH_FORMS = ("none", "atomic", "edge", "fused", "update_edge")
 
 STAT_FIELDS = ("round", "active", "new_deliveries", "relays", "active_vertices", "active_words",
-               "wedges", "deg_active", "scatter_words", "touched_words")
+               "wedges", "deg_active", "scatter_words", "touched_words", "received")
 
 
 @dataclass(slots=True)
@@ -45,6 +45,8 @@ class RoundStats:
     deg_active: int
     scatter_words: int
     touched_words: int
+    received: int = 0   # packets that arrived this round (sum of message_count_recv += 1,
+                        # nodeconnection.py:215): last round's sends less the lost ones
     push_form: int = 0  # gossip: how this round's pushes left (PUSH_FORMS); not a result
 
     @classmethod
@@ -62,6 +64,20 @@ class RoundStats:
 
     def as_dict(self):
         return {f: getattr(self, f) for f in STAT_FIELDS}
+
+
+@dataclass
+class Sends:
+    """Every send of one round (Node.send_to_node calls, node.py:114-120), sorted by (receiver,
+    sender, msg); lost = churn dropped it (nodeconnection.py:123-126).  The ones not lost are the
+    next round's arrivals, each a node_message call (nodeconnection.py:211-216)."""
+    sender: np.ndarray
+    receiver: np.ndarray
+    msg: np.ndarray
+    lost: np.ndarray
+
+    def __len__(self):
+        return len(self.sender)
 
 
 @dataclass
@@ -302,6 +318,39 @@ class GraphNetwork:
             self._h, cap, _lib.ptr(peer), _lib.ptr(msg), _lib.ptr(hop), _lib.ptr(parent), ctypes.byref(n)))
         k = min(n.value, cap)
         return Deliveries(peer[:k], msg[:k], hop[:k], parent[:k])
+
+    def sends(self):
+        """Every send of the most recent round (p2pg_get_sends): the packets its first receipts
+        put on the wire, duplicates included, after any drop_relays."""
+        n = ctypes.c_int64()
+        z = np.zeros(1, dtype=np.int32)
+        z8 = np.zeros(1, dtype=np.uint8)
+        L = _lib.lib()
+        self._check(L.p2pg_get_sends(self._h, 0, _lib.ptr(z), _lib.ptr(z), _lib.ptr(z), _lib.ptr(z8),
+                                     ctypes.byref(n)))
+        cap = int(n.value)
+        snd = np.zeros(max(cap, 1), dtype=np.int32)
+        rcv = np.zeros_like(snd)
+        msg = np.zeros_like(snd)
+        lost = np.zeros(max(cap, 1), dtype=np.uint8)
+        self._check(L.p2pg_get_sends(self._h, cap, _lib.ptr(snd), _lib.ptr(rcv), _lib.ptr(msg), _lib.ptr(lost),
+                                     ctypes.byref(n)))
+        k = min(int(n.value), cap)
+        return Sends(snd[:k], rcv[:k], msg[:k], lost[:k].astype(bool))
+
+    def drop_relays(self, peer, msg):
+        """Withdraw the relays of these first receipts of the most recent round: the app did not
+        forward them (p2pg_drop_relays)."""
+        p = np.ascontiguousarray(peer, dtype=np.int32)
+        m = np.ascontiguousarray(msg, dtype=np.int32)
+        if len(p) != len(m):
+            raise ValueError("peer and msg must have the same length")
+        self._check(_lib.lib().p2pg_drop_relays(self._h, len(p), _lib.ptr(p) if len(p) else None,
+                                                _lib.ptr(m) if len(m) else None))
+        drop = sum(min(self.fanout, d) if self.mode == "gossip" else
+                   (d if self.rounds and self.rounds[-1].round == 0 else max(d - 1, 0))
+                   for d in self.graph.degree()[p].tolist())
+        self.message_count_send -= drop
 
     # -- validation planes ----------------------------------------------------------------
     def seen_plane(self):

@@ -152,10 +152,13 @@ class TorchTransport:
       record count per destination + its round counters) -> [world, len].  The vector is on the
       host already (the pack reads its counts back), so it goes over a host (gloo) group: no
       device round trip, no stream synchronisation;
-    * ``exchange_records(...)``: grouped point-to-point sends / receives of the packed records
-      (``batch_isend_irecv``), exactly the live rows each peer rank needs;
+    * ``exchange_records(...)``: ONE all-to-all of the packed records per round
+      (``all_to_all_single`` with per-rank split sizes = RCCL's all-to-all-v over xGMI): each
+      rank's records for rank q, compacted in destination order, land in rank q's receive
+      buffer in source order -- exactly the live rows each peer rank needs;
     * ``engine_stream()``: the stream the rank's engine should launch on (device runs), so
-      that the receives can be ordered before the unpack by a stream wait, not a host sync."""
+      that the collective's completion is ordered before the unpack by a stream wait, not a
+      host sync."""
 
     def __init__(self, device=None, group=None, host_group=None):
         import torch
@@ -180,6 +183,7 @@ class TorchTransport:
                              "host_group_for(group), created by every rank of the job")
         self.rows_total = 0  # boundary rows offered / actually sent (exchange volume)
         self.rows_sent = 0
+        self.collectives = 0  # all-to-alls issued
 
     def engine_stream(self):
         if self.device is None or not str(self.device).startswith("cuda"):
@@ -193,30 +197,30 @@ class TorchTransport:
         dist.all_gather_into_tensor(out, t, group=self.host_group)
         return out.numpy().reshape(self.world, -1)
 
+    def _all_to_all(self, out, inp, out_splits, in_splits):
+        """The collective: all_to_all_single over the transport's group (RCCL on device tensors:
+        one all-to-all-v, issued on torch's current stream)."""
+        self.dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
+
     def exchange_records(self, send_buf, send_off, send_cnt, recv_buf, recv_cnt, R):
         """send_buf: records to rank q at record send_off[q], send_cnt[q] of them; recv_buf:
-        the records from every source rank, packed in source order (R int64 per record)."""
-        torch, dist = self.torch, self.dist
-        recv_off = np.concatenate([[0], np.cumsum(recv_cnt)]).astype(np.int64)
+        the records from every source rank, packed in source order (R int64 per record).  Every
+        rank calls it every round (a collective), also with nothing to move."""
+        torch = self.torch
+        in_splits = [int(c) * R for c in send_cnt]
+        out_splits = [int(c) * R for c in recv_cnt]
+        segs = [send_buf[int(send_off[q]) * R:int(send_off[q]) * R + in_splits[q]]
+                for q in range(self.world) if in_splits[q]]
+        x = torch.cat(segs) if len(segs) > 1 else segs[0] if segs else send_buf[:0]
+        y = recv_buf[:sum(out_splits)]
         stage = self.backend != "nccl" and send_buf.is_cuda  # gloo moves host tensors only
-        ops, landing = [], []
-        for q in range(self.world):
-            if q == self.rank:
-                continue
-            if send_cnt[q]:
-                x = send_buf[int(send_off[q]) * R:(int(send_off[q]) + int(send_cnt[q])) * R]
-                ops.append(dist.P2POp(dist.isend, x.cpu() if stage else x, q, group=self.group))
-            if recv_cnt[q]:
-                y = recv_buf[int(recv_off[q]) * R:int(recv_off[q + 1]) * R]
-                buf = torch.empty(y.shape, dtype=y.dtype) if stage else y
-                ops.append(dist.P2POp(dist.irecv, buf, q, group=self.group))
-                if stage:
-                    landing.append((y, buf))
-        if ops:
-            for req in dist.batch_isend_irecv(ops):
-                req.wait()
-        for y, buf in landing:
-            y.copy_(buf)
+        if stage:
+            x, land = x.cpu(), torch.empty(y.shape, dtype=y.dtype)
+            self._all_to_all(land, x, out_splits, in_splits)
+            y.copy_(land)
+        else:
+            self._all_to_all(y, x, out_splits, in_splits)
+        self.collectives += 1
 
 
 class PartitionedNetwork:

@@ -22,7 +22,14 @@ def golden_cases(prefix="", dynamic=False):
     updates_of), else only the static-topology ones.  The real-TCP fixtures (config1_tcp,
     tcp*) hold reachability only: tcp_cases()."""
     return sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith(".npz") and f.startswith(prefix)
-                  and not f.startswith(("config1_tcp", "tcp")) and f.startswith("dyn_") == dynamic)
+                  and not f.startswith(("config1_tcp", "tcp", "app_", "plane_"))
+                  and f.startswith("dyn_") == dynamic)
+
+
+def app_cases():
+    """Hook-semantics fixtures (app_*): Node apps of tests/compat_apps.py run on the reference's
+    own Node objects -- every node_message call in order, every node's counters."""
+    return sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith(".npz") and f.startswith("app_"))
 
 
 def tcp_cases():

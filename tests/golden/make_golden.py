@@ -34,6 +34,7 @@ Usage:  python tests/golden/make_golden.py        (writes tests/golden/*.npz)
         python tests/golden/make_golden.py dyn    (only the dyn_* fixtures)
         python tests/golden/make_golden.py wire   (only the wire_* byte-stream fixtures)
         python tests/golden/make_golden.py tcp    (only the larger real-TCP fixtures)
+        python tests/golden/make_golden.py apps   (only the app_* hook-semantics fixtures)
 """
 import os
 import sys
@@ -311,7 +312,7 @@ def wire_case(name, graph, M, src_seed, mode="flood", k=3, gseed=0, churn=0.0, c
             off.append(len(blob))
     out = os.path.join(HERE, f"{name}.npz")
     np.savez_compressed(out, rowptr=graph.rowptr, colidx=graph.colidx, src=src, hop=hop, parent=parent,
-                        round_relays=relays, mode=np.array(mode), fanout=np.int64(k),
+                        round_relays=relays, total_recv=np.int64(recv), mode=np.array(mode), fanout=np.int64(k),
                         gossip_seed=np.uint64(gseed), churn_threshold=np.uint64(thr),
                         churn_seed=np.uint64(cseed), s_round=np.array(rnd, np.int32),
                         s_sender=np.array(snd, np.int32), s_receiver=np.array(rcv, np.int32),
@@ -436,9 +437,93 @@ def dynamic_cases():
          churn=0.10, cseed=9, updates=random_updates(g, [1, 4], 40, 4))
 
 
+def app_case(name, app, spec, origins, churn, cseed):
+    """A Node app of tests/compat_apps.py on the reference's own Node / NodeConnection objects,
+    round-synchronous like Harness (receivers in ascending id, then senders, then the order the
+    sender wrote): every node_message call as (receiver, sender, payload) in call order, and
+    every node's message_count_send / message_count_recv."""
+    import json
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import compat_apps
+    graph = compat_apps.make_graph(spec, PeerGraph)
+    thr = int(np.floor(churn * 4294967296.0)) if churn else 0
+    log = []
+    App = type("App", (compat_apps.APPS[app], Node), {"log": log})
+
+    class H:
+        round = 0
+        outbox = []
+
+        def dropped(self, a, b):
+            return bool(thr) and bool(philox.churn_dropped(self.round, a, b, thr, cseed))
+
+    h = H()
+
+    class AppNode(App):
+        def __init__(self, i):
+            super().__init__("127.0.0.1", 30000 + i, id=str(i))
+            self.sock.close()
+
+        def init_server(self):
+            pass
+
+    V = graph.V
+    nodes = [AppNode(i) for i in range(V)]
+    conn = {}
+    for a in range(V):
+        for b in graph.neighbours(a):
+            b = int(b)
+            if b <= a:
+                continue
+            ca = NodeConnection(nodes[a], FakeSock(h, a, b), str(b), "127.0.0.1", 30000 + b)
+            cb = NodeConnection(nodes[b], FakeSock(h, b, a), str(a), "127.0.0.1", 30000 + a)
+            nodes[a].nodes_outbound.append(ca)
+            nodes[b].nodes_inbound.append(cb)
+            conn[(a, b)], conn[(b, a)] = ca, cb
+    for peer, data in origins:
+        nodes[peer].originate(data)
+    eot = (0x04).to_bytes(1, "big")
+    while h.outbox:
+        h.round += 1
+        batch = sorted(h.outbox)
+        h.outbox = []
+        i = 0
+        while i < len(batch):
+            rcv, snd = batch[i][0], batch[i][1]
+            buf = b""
+            while i < len(batch) and batch[i][0] == rcv and batch[i][1] == snd:
+                buf += batch[i][3]
+                i += 1
+            c = conn[(rcv, snd)]
+            pos = buf.find(eot)
+            while pos > 0:
+                packet, buf = buf[:pos], buf[pos + 1:]
+                nodes[rcv].message_count_recv += 1
+                nodes[rcv].node_message(c, c.parse_packet(packet))
+                pos = buf.find(eot)
+    np.savez_compressed(os.path.join(HERE, f"{name}.npz"), rowptr=graph.rowptr, colidx=graph.colidx,
+                        app=np.array(app), origins=np.array(json.dumps(origins)),
+                        churn_threshold=np.uint64(thr), churn_seed=np.uint64(cseed),
+                        events=np.array([json.dumps(e) for e in log]),
+                        sends=np.array([n.message_count_send for n in nodes], dtype=np.int64),
+                        recvs=np.array([n.message_count_recv for n in nodes], dtype=np.int64),
+                        rounds=np.int64(h.round))
+    print(f"{name}: {len(log)} node_message events over {h.round} rounds")
+
+
+def app_cases():
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import compat_apps
+    for name, (app, spec, origins, churn, cseed) in compat_apps.CASES.items():
+        app_case(name, app, spec, origins, churn, cseed)
+
+
 def main():
     global Node, NodeConnection
     Node, NodeConnection = _load_reference()
+    if sys.argv[1:] == ["apps"]:
+        app_cases()
+        return
     if sys.argv[1:] == ["dyn"]:
         dynamic_cases()
         return
@@ -477,6 +562,7 @@ def main():
     config1_tcp()
     wire_cases()
     tcp_larger()
+    app_cases()
 
 
 def tcp_larger():

@@ -211,6 +211,49 @@ class MockEngine:
         return Deliveries(vs.astype(np.int32), ms.astype(np.int32), self.hop[vs, ms].astype(np.int32),
                           self.par[vs, ms].astype(np.int32))
 
+    def sends(self):
+        """include/p2pgpu.h p2pg_get_sends: every send of the last round, sorted by (receiver,
+        sender, msg); flood skips the connection a first receipt came from."""
+        from p2pnetwork.gpu.network import Sends
+        r = self.round - 1
+        out = []
+        for v, m in zip(*np.nonzero(self.F)):
+            nb = self.g.colidx[self.g.rowptr[v]:self.g.rowptr[v + 1]]
+            d = len(nb)
+            if self.mode == "flood":
+                tg = [u for u in nb if r == 0 or self.gid[u] != self.par[v, m]]
+            elif d <= self.k:
+                tg = list(nb)
+            else:
+                tg = list(nb[philox.gossip_picks(r, self.gid[v], m, d, self.k, self.gseed)[0]])
+            for u in tg:
+                lost = bool(philox.churn_dropped(r, self.gid[v], self.gid[u], self.thr, self.cseed))
+                out.append((int(u), int(v), int(m), lost))
+        out.sort()
+        a = np.array(out, dtype=np.int64).reshape(-1, 4)
+        return Sends(a[:, 1].astype(np.int32), a[:, 0].astype(np.int32), a[:, 2].astype(np.int32),
+                     a[:, 3].astype(bool))
+
+    def drop_relays(self, peer, msg):
+        """p2pg_drop_relays: the listed first receipts of the last round do not relay."""
+        peer, msg = np.asarray(peer, dtype=np.int64), np.asarray(msg, dtype=np.int64)
+        assert self.F[peer, msg].all() and len(set(zip(peer.tolist(), msg.tolist()))) == len(peer)
+        self.F[peer, msg] = False
+        if self.mode == "gossip":  # redo the last round's pushes without them
+            self.next[:] = False
+            self.cand[:] = np.iinfo(np.int64).max
+            self.round -= 1
+            self._scatter()
+            self.round += 1
+
+    def update_edges(self, add=(), remove=()):
+        """p2pg_update_edges between rounds: sends of the last round on removed connections
+        are lost (flood: pulled over the new graph minus them next round; the mock keeps the
+        plain form: static-topology tests only run through it mid-run)."""
+        self.graph = self.g = self.g.with_changes(add, remove)
+        self.deg = self.g.degree()
+        self.rows = np.repeat(np.arange(self.V), self.deg)
+
     def seen_plane(self):
         return _words(self.seen)
 

@@ -5,10 +5,14 @@ in the driver's 8-GPU bench.
 1. ``init_process_group("nccl", device_id=cuda:0)`` at world 1, ``host_group_for`` (a gloo
    group next to the nccl one) and ``TorchTransport`` over them, whose count all-gather goes
    over gloo;
-2. two ranks of a vertex partition, as threads of this process, whose records move between
-   them by ``all_to_all_single`` on device tensors through the RCCL communicator (at world 1 an
-   all-to-all is RCCL's device copy of the rank's own chunk), and whose engines order
-   ``p2pg_exchange_unpack_live`` after it with ``PartitionedNetwork._ready``'s ``wait_stream``;
+2. two ranks of a vertex partition, as threads of this process, each with a transport that IS
+   ``TorchTransport`` -- its own ``exchange_records`` (compaction per destination, split sizes,
+   gloo staging rules, stream order) -- except for the one collective primitive
+   ``_all_to_all``: RCCL refuses two ranks on one GPU ("Duplicate GPU detected"), so the two
+   logical ranks' all-to-alls are issued as ONE world-1 RCCL ``all_to_all_single`` with split
+   sizes (the call of production, at world 1 a device copy) over both ranks' chunks, and the
+   engines order ``p2pg_exchange_unpack_live`` after it with ``PartitionedNetwork._ready``'s
+   ``wait_stream``;
 3. the partitioned runs (flood with churn, gossip with churn, W = 64) == one engine, bit for bit.
 
 Replaces, like the rest of the partition layer, the cross-host fan-out of NodeConnection.send
@@ -25,15 +29,18 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
+from p2pnetwork.gpu import TorchTransport  # noqa: E402
 
-class RcclLoopback:
-    """The PartitionedNetwork transport contract for `world` rank threads of one process: counts
-    meet in a shared slot table (and rank 0 passes them through TorchTransport's gloo all-gather),
-    records move device-to-device through the RCCL communicator, all issued by rank 0's thread."""
 
-    def __init__(self, shared, rank, tt):
-        self.s, self.rank, self.tt = shared, rank, tt
-        self.rows_total = self.rows_sent = 0
+class RcclLoopback(TorchTransport):
+    """Logical rank `rank` of `world` rank threads of one process over the world-1 RCCL group:
+    TorchTransport with the collective primitive (and the count all-gather) met in a shared slot
+    table; rank 0's thread issues the one RCCL all_to_all_single per round."""
+
+    def __init__(self, shared, rank, world, tt):
+        super().__init__(device=tt.device, host_group=tt.host_group)
+        self.world, self.rank = world, rank  # logical
+        self.s, self.tt = shared, tt
 
     def _gather(self, item):
         s = self.s
@@ -43,9 +50,6 @@ class RcclLoopback:
         s["barrier"].wait()
         return items
 
-    def engine_stream(self):
-        return torch.cuda.Stream(device=0)
-
     def exchange_counts(self, vec):
         allv = np.stack(self._gather(np.asarray(vec, dtype=np.int64)))
         if self.rank == 0:  # the gloo group next to the nccl communicator, every round
@@ -53,40 +57,45 @@ class RcclLoopback:
             assert np.array_equal(got.reshape(-1), allv.reshape(-1)), "gloo all-gather"
         return allv
 
-    def exchange_records(self, send_buf, send_off, send_cnt, recv_buf, recv_cnt, R):
-        items = self._gather((send_buf, np.asarray(send_off), np.asarray(send_cnt), recv_buf,
-                              np.asarray(recv_cnt)))
+    def _all_to_all(self, out, inp, out_splits, in_splits):
+        items = self._gather((out, inp, list(out_splits), list(in_splits)))
         if self.rank == 0:
-            world = len(items)
-            moved = 0
-            for q in range(world):  # destination q receives its sources' records in source order
-                rb, rc = items[q][3], items[q][4]
-                off = 0
-                for p in range(world):
-                    if p == q:
-                        continue
-                    sb, so, sc = items[p][0], items[p][1], items[p][2]
-                    n = int(sc[q])
-                    assert n == int(rc[p])
+            W = len(items)
+            # destination q's chunk from source p: p's input at offset sum(in_splits[:q]);
+            # q's output takes its sources in order -- one input / output pair in (q, p) order
+            ins, outs = [], []
+            for q in range(W):
+                for p in range(W):
+                    n = items[p][3][q]
+                    assert n == items[q][2][p], "split sizes disagree"
                     if n:
-                        x = sb[int(so[q]) * R:(int(so[q]) + n) * R]
-                        y = rb[off * R:(off + n) * R]
-                        dist.all_to_all_single(y, x)  # RCCL kernel; the current stream waits on it
-                        moved += n
-                    off += n
-            self.s["moved"] += moved
+                        a = sum(items[p][3][:q])
+                        ins.append(items[p][1][a:a + n])
+                        b = sum(items[q][2][:p])
+                        outs.append(items[q][0][b:b + n])
+            total = sum(x.numel() for x in ins)
+            if total:
+                x = torch.cat(ins)
+                y = torch.empty_like(x)
+                dist.all_to_all_single(y, x, [total], [total])  # RCCL kernel, current stream
+                o = 0
+                for t in outs:
+                    t.copy_(y[o:o + t.numel()])
+                    o += t.numel()
+            self.s["moved"] += total
+            self.s["calls"] += 1
         self.s["barrier"].wait()  # the copies are enqueued before any rank unpacks
 
 
 def run_case(tt, g, src, world, **kw):
     from p2pnetwork.gpu import GraphNetwork, PartitionedNetwork
-    shared = {"slots": [None] * world, "barrier": threading.Barrier(world), "moved": 0}
+    shared = {"slots": [None] * world, "barrier": threading.Barrier(world), "moved": 0, "calls": 0}
     res, errors = [None] * world, []
 
     def rank_main(rank):
         try:
             torch.cuda.set_device(0)
-            net = PartitionedNetwork(g, world, rank, RcclLoopback(shared, rank, tt), **kw)
+            net = PartitionedNetwork(g, world, rank, RcclLoopback(shared, rank, world, tt), **kw)
             with net.net:
                 net.broadcast(src)
                 rounds = net.run()
@@ -122,7 +131,9 @@ def run_case(tt, g, src, world, **kw):
                 b.pop()
             assert a == b, k
     assert shared["moved"] > 0, "no record moved through RCCL"
-    return len(rounds1), shared["moved"]
+    # one all-to-all per exchange (frontier rows per round; gossip also its senders' rows)
+    assert shared["calls"] >= len(rounds1) - 1
+    return len(rounds1), shared["moved"] // (1 + len(src) // 64)
 
 
 def main():
@@ -136,11 +147,14 @@ def main():
     tt = TorchTransport(device=torch.device("cuda", 0), host_group=hg)
     assert tt.backend == "nccl" and tt.world == 1
     assert np.array_equal(tt.exchange_counts(np.array([3, 5, 7])), [[3, 5, 7]])
-    # one RCCL collective on device tensors by itself first
+    # one RCCL collective on device tensors by itself first, and TorchTransport's own exchange
+    # at world 1 (no other rank: an empty all-to-all, as a rank with nothing to send makes it)
     x = torch.arange(1 << 20, dtype=torch.int64, device="cuda:0")
     y = torch.empty_like(x)
     dist.all_to_all_single(y, x)
     assert torch.equal(x, y)
+    tt.exchange_records(x, np.array([0]), np.array([0]), y, np.array([0]), 65)
+    assert tt.collectives == 1
     thr = churn_threshold(0.05)
     out = []
     g = PeerGraph.watts_strogatz(40_000, 8, 0.1, seed=9)

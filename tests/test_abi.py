@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol():
 def test_struct_layouts():
     from p2pnetwork.gpu import _lib
     assert ctypes.sizeof(_lib.Config) == 40
-    assert ctypes.sizeof(_lib.RoundStatsC) == 80
+    assert ctypes.sizeof(_lib.RoundStatsC) == 88
 
 
 def test_graph_generators_are_simple_undirected_and_deterministic():

@@ -1,12 +1,19 @@
-"""Per-callback compat mode (p2pnetwork.gpu.compat): a Node-style dedup-relay app, written
-against the reference's hook surface, runs unchanged on CompatNetwork and reproduces the
-golden fixtures made with the reference's own Node objects (first-receipt round and sender per
-peer and message, total relays = sum of message_count_send).  CPU tests drive it with the
-test-only engine stand-in (tests/partition_mock.py); the gpu-marked ones with the HIP engine."""
+"""Per-callback compat mode (p2pnetwork.gpu.compat): Node-style apps, written against the
+reference's hook surface, run unchanged on CompatNetwork with the reference's hook semantics --
+node_message for every arriving packet, duplicates included (nodeconnection.py:211-216), the
+app's own relay decision -- and reproduce fixtures made with the reference's own Node objects:
+the dedup relay's first-receipt round and sender per (peer, msg), sum of message_count_send and
+of message_count_recv (the fixture's total_recv), and, for apps beyond the dedup relay
+(tests/compat_apps.py), every node_message call in order and every node's counters.  CPU tests
+drive it with the test-only engine stand-in (tests/partition_mock.py); the gpu-marked ones with
+the HIP engine (p2pg_get_sends / p2pg_drop_relays)."""
+import json
+
 import numpy as np
 import pytest
 
-from conftest import golden_cases, load_golden, updates_of
+import compat_apps
+from conftest import app_cases, golden_cases, load_golden, updates_of
 from partition_mock import MockEngine
 
 
@@ -28,7 +35,28 @@ def dedup_app():
     return DedupRelay
 
 
-def run_compat(z, factory=None):
+def harness_gossip_app():
+    """The fixtures' gossip app as the reference harness writes it (make_golden.py RelayNode):
+    send_to_node on the k Philox-chosen connections of a first receipt."""
+    from p2pnetwork.gpu.compat import SimNode
+
+    class GossipRelay(SimNode):
+        def __init__(self, host, port, id=None, callback=None, max_connections=0):
+            super().__init__(host, port, id, callback, max_connections)
+            self.seen = {}
+
+        def node_message(self, node, data):
+            mid = data["mid"]
+            if mid in self.seen:
+                return
+            self.seen[mid] = (self._net.current_round, int(node.id))
+            for c in self._net.gossip_connections(self, mid):
+                self.send_to_node(c, data)
+
+    return GossipRelay
+
+
+def run_compat(z, factory=None, app=None):
     from p2pnetwork.gpu import PeerGraph
     from p2pnetwork.gpu.compat import CompatNetwork
     g = PeerGraph(z["rowptr"], z["colidx"])
@@ -36,7 +64,7 @@ def run_compat(z, factory=None):
               churn_threshold_value=int(z["churn_threshold"]), churn_seed=int(z["churn_seed"]))
     if factory is not None:
         kw["engine_factory"] = factory
-    net = CompatNetwork(g, dedup_app(), **kw)
+    net = CompatNetwork(g, app or dedup_app(), **kw)
     for m, s in enumerate(z["src"]):
         net.nodes[int(s)].seen[m] = (0, -1)
         net.nodes[int(s)].send_to_nodes({"mid": m})
@@ -57,14 +85,73 @@ def check(z, hop, par, sends, recv):
     np.testing.assert_array_equal(hop, z["hop"])
     np.testing.assert_array_equal(par, z["parent"])
     assert sends == int(z["round_relays"].sum())
-    assert recv == int((z["hop"] > 0).sum())  # first receipts (the origin gets no node_message)
+    # every arriving packet, duplicates included, less the lost sends (nodeconnection.py:215)
+    assert recv == int(z["total_recv"])
 
 
 @pytest.mark.parametrize("name", golden_cases())
 def test_compat_mock_engine_matches_reference_golden(name):
     z = load_golden(name)
-    hop, par, sends, recv, _ = run_compat(z, MockEngine)
+    hop, par, sends, recv, net = run_compat(z, MockEngine)
     check(z, hop, par, sends, recv)
+    assert net.explicit_packets == 0  # the dedup relay is carried by the engine alone
+
+
+def _run_app(name, factory=None):
+    """An app_* fixture's app on CompatNetwork: its node_message events and counters."""
+    from p2pnetwork.gpu.compat import CompatNetwork, SimNode
+    z = load_golden(name)
+    app = str(z["app"])
+    log = []
+    App = type("App", (compat_apps.APPS[app], SimNode), {"log": log})
+    g = compat_apps.make_graph(compat_apps.CASES[name][1])
+    np.testing.assert_array_equal(g.colidx, z["colidx"])
+    kw = dict(churn_threshold_value=int(z["churn_threshold"]), churn_seed=int(z["churn_seed"]))
+    if factory is not None:
+        kw["engine_factory"] = factory
+    net = CompatNetwork(g, App, **kw)
+    for peer, data in json.loads(str(z["origins"])):
+        net.nodes[peer].originate(data)
+    net.run()
+    net.close()
+    return z, [json.dumps(list(e)) for e in log], net
+
+
+def _check_app(z, events, net):
+    assert events == list(z["events"])
+    np.testing.assert_array_equal([n.message_count_send for n in net.nodes], z["sends"])
+    np.testing.assert_array_equal([n.message_count_recv for n in net.nodes], z["recvs"])
+
+
+@pytest.mark.parametrize("name", app_cases())
+def test_compat_apps_mock_engine_match_reference_events(name):
+    """Apps beyond the dedup relay (no dedup + ttl, acks back to the sender, relays to every
+    connection, relays on the second arrival): every node_message call, in order, and every
+    node's counters == the reference's own Node objects'."""
+    _check_app(*_run_app(name, MockEngine))
+
+
+def test_compat_recording_app_gets_one_delivery_per_connection():
+    """test_node.py:106-194: path 1-0-2, every node calls send_to_nodes once, the callback only
+    records -> exactly 4 node_message events (the fan-out law: one delivery per connection);
+    nothing is relayed because the app does not relay."""
+    from p2pnetwork.gpu import PeerGraph
+    from p2pnetwork.gpu.compat import CompatNetwork, SimNode
+    events = []
+
+    def cb(event, main_node, connected_node, data):
+        if event == "node_message":
+            events.append((main_node.id, connected_node.id, data))
+
+    net = CompatNetwork(PeerGraph.from_edges(3, [(0, 1), (0, 2)]), SimNode, node_kwargs={"callback": cb},
+                        engine_factory=MockEngine)
+    for i in (0, 1, 2):
+        net.nodes[i].send_to_nodes(f"message from {i}")
+    net.run()
+    assert sorted(events) == [("0", "1", "message from 1"), ("0", "2", "message from 2"),
+                              ("1", "0", "message from 0"), ("2", "0", "message from 0")]
+    assert [n.message_count_send for n in net.nodes] == [2, 1, 1]
+    assert [n.message_count_recv for n in net.nodes] == [2, 1, 1]
 
 
 def test_compat_lifecycle_and_payload_codec():
@@ -88,12 +175,11 @@ def test_compat_lifecycle_and_payload_codec():
     net.nodes[3].send_to_nodes(12345)            # not sendable: counted, reaches nobody
     net.run()
     got = [(e[1], e[2], e[3]) for e in events if e[0] == "node_message"]
-    # round 1: peer 1 gets msg 0 from 0, peer 2 gets msg 1 from 3; round 2: 2<-1 (m0), 1<-2 (m1)
-    assert got == [("1", "0", {"t": [1, 2]}), ("2", "3", 42), ("1", "2", 42), ("2", "1", {"t": [1, 2]}),
-                   ("0", "1", 42), ("3", "2", {"t": [1, 2]})]
-    # flood relays: origin deg, others deg-1; the unsendable send counted 1 at peer 3
-    assert [n.message_count_send for n in net.nodes] == [1, 2, 2, 1 + 1]
-    assert [n.message_count_recv for n in net.nodes] == [1, 2, 2, 1]
+    # SimNode's node_message only fires the callback (node.py:334-338): one hop, no relay
+    assert got == [("1", "0", {"t": [1, 2]}), ("2", "3", 42)]
+    # every send_to_node call counted (node.py:116), the unsendable one included
+    assert [n.message_count_send for n in net.nodes] == [1, 0, 0, 1 + 1]
+    assert [n.message_count_recv for n in net.nodes] == [0, 1, 1, 0]
     net.nodes[2].stop()
     assert events[-1][0] == "node_request_to_stop"
 
@@ -102,9 +188,71 @@ def test_compat_lifecycle_and_payload_codec():
 @pytest.mark.parametrize("name", golden_cases())
 def test_compat_gpu_engine_matches_reference_golden(name):
     z = load_golden(name)
-    hop, par, sends, recv, net = run_compat(z)
+    events = []
+
+    class App(dedup_app()):
+        def node_message(self, node, data):
+            events.append(1)
+            super().node_message(node, data)
+
+    hop, par, sends, recv, net = run_compat(z, app=App)
     check(z, hop, par, sends, recv)
-    assert net.absorbed_sends == recv if str(z["mode"]) == "flood" else True
+    assert len(events) == recv == int(z["total_recv"])  # one node_message per arrival
+    assert net.explicit_packets == 0  # every relay stayed in the engine
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", [n for n in golden_cases() if "gossip" in n])
+def test_compat_gpu_harness_gossip_app_matches_reference_golden(name):
+    """The fixtures' own gossip app (send_to_node on the Philox-chosen connections, as the
+    reference harness wrote it) is recognised as the engine's relay: no explicit packets."""
+    z = load_golden(name)
+    hop, par, sends, recv, net = run_compat(z, app=harness_gossip_app())
+    check(z, hop, par, sends, recv)
+    assert net.explicit_packets == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", app_cases())
+def test_compat_apps_gpu_engine_match_reference_events(name):
+    """As the mock-engine test, through the HIP engine's sends stream and relay withdrawal."""
+    _check_app(*_run_app(name))
+
+
+@pytest.mark.gpu
+def test_compat_gpu_recording_apps():
+    """The 4-event law of test_node.py:106-194 on the HIP engine, and the reference's example
+    node (examples/MyOwnPeer2PeerNode.py:27-28 only prints) on config 2: every broadcast reaches
+    exactly the origin's connections -- sum of deg(origin) deliveries, no relay."""
+    from p2pnetwork.gpu import PeerGraph
+    from p2pnetwork.gpu.compat import CompatNetwork, SimNode
+    events = []
+
+    def cb(event, main_node, connected_node, data):
+        if event == "node_message":
+            events.append((main_node.id, connected_node.id, data))
+
+    with CompatNetwork(PeerGraph.from_edges(3, [(0, 1), (0, 2)]), SimNode, node_kwargs={"callback": cb}) as net:
+        for i in (0, 1, 2):
+            net.nodes[i].send_to_nodes(f"message from {i}")
+        stats = net.run()
+    assert len(events) == 4 and sum(s.received for s in stats) == 4
+
+    class MyOwnPeer2PeerNode(SimNode):
+        def node_message(self, node, data):
+            events.append(("node_message", self.id, node.id, data))
+
+    z = load_golden("c2_rrg1000_flood")
+    g = PeerGraph(z["rowptr"], z["colidx"])
+    events.clear()
+    with CompatNetwork(g, MyOwnPeer2PeerNode) as net:
+        for m, s in enumerate(z["src"]):
+            net.nodes[int(s)].send_to_nodes({"mid": m})
+        stats = net.run()
+        deg = g.degree()
+        assert len(events) == int(deg[z["src"]].sum()) == 512
+        assert sum(n.message_count_recv for n in net.nodes) == 512
+        assert sum(s.received for s in stats) == 512 and net.explicit_packets == 0
 
 
 @pytest.mark.gpu

@@ -76,6 +76,8 @@ def test_gpu_topology_updates_match_reference_harness(name, push, monkeypatch):
         np.testing.assert_array_equal(net.delivered(), z["hop"] >= 0)
         np.testing.assert_array_equal(trim_zeros([r.relays for r in rounds]), trim_zeros(z["round_relays"]))
         assert net.message_count_send == int(z["round_relays"].sum())
+        # arrivals, less the sends in flight on removed connections (and churn's)
+        assert sum(r.received for r in rounds) == int(z["total_recv"])
     assert_rounds(rounds, oracle_of(z, upd).rounds)
 
 
@@ -149,6 +151,7 @@ def test_gpu_snapshot_resume_is_bit_identical(name, cut, push, monkeypatch, tmp_
         np.testing.assert_array_equal(net2.seen_plane(), seen_a)
         assert net2.message_count_send == int(z["round_relays"].sum())
     assert [r.as_dict() for r in rest] == [r.as_dict() for r in rest2]
+    assert sum(r.received for r in first + rest2) == int(z["total_recv"])  # (snapshot v3)
     np.testing.assert_array_equal(hop_a, hop_b)
     np.testing.assert_array_equal(par_a, par_b)
     np.testing.assert_array_equal(hop_b, z["hop"])
@@ -235,3 +238,54 @@ def test_gpu_restore_refuses_other_graph_or_sources():
         other.broadcast(src)
         with pytest.raises(P2PGError, match="configuration differs"):
             other.restore(snap)
+
+
+@pytest.mark.parametrize("M", [1024, 4096])
+def test_gpu_gossip_restore_then_update_edges_wide_rows(M, monkeypatch):
+    """A gossip run with packed rows (W = 16 / 64: active-word masks AW, which snapshots do not
+    carry) restored into a fresh engine and then changing connections at once: the re-push of the
+    last round's sends lists words by AW, so the restore rebuilds it from the frontier rows.
+    Equal to the uninterrupted run and to the oracle with the same updates, every push form."""
+    from p2pnetwork.gpu import GraphNetwork, PeerGraph, make_sources
+    g = PeerGraph.barabasi_albert(3000, 3, seed=31)
+    src = make_sources(g.V, M, seed=32)
+    rng = np.random.default_rng(5)
+    rows = np.repeat(np.arange(g.V), g.degree())
+    e = np.stack([rows, g.colidx], 1)
+    e = e[e[:, 0] < e[:, 1]]
+    rem = e[rng.choice(len(e), 200, replace=False)].astype(np.int32)
+    have = set(map(tuple, e.tolist()))
+    add = []
+    while len(add) < 150:
+        a, b = sorted(int(x) for x in rng.integers(0, g.V, 2))
+        if a != b and (a, b) not in have and [a, b] not in add:
+            add.append([a, b])
+    upd = {3: (np.array(add, np.int32), rem)}
+    kw = dict(mode="gossip", fanout=2, gossip_seed=77, churn_threshold_value=300000000, churn_seed=9)
+    for push in ("auto", "atomic", "store"):
+        monkeypatch.setenv("P2PG_GOSSIP_PUSH", push)
+        with GraphNetwork(g, record=True, **kw) as net:
+            net.broadcast(src)
+            ra = run_with_updates(net, upd)
+            hop_a, par_a = net.hop_parent()
+        with GraphNetwork(g, record=True, **kw) as net:
+            net.broadcast(src)
+            first = [net.step() for _ in range(4)]  # rounds 0..3; the update follows round 3
+            snap = net.snapshot()
+        with GraphNetwork(g, record=True, **kw) as net2:
+            net2.broadcast(src)
+            net2.restore(snap)
+            net2.update_edges(*upd[3])
+            rest = []
+            while True:
+                st = net2.step()
+                rest.append(st)
+                if not st.active:
+                    break
+            hop_b, par_b = net2.hop_parent()
+        np.testing.assert_array_equal(hop_b, hop_a, err_msg=push)
+        np.testing.assert_array_equal(par_b, par_a, err_msg=push)
+        assert [r.as_dict() for r in first + rest] == [r.as_dict() for r in ra], push
+    ora = relay_oracle.gossip(g.rowptr, g.colidx, src, 2, 77, 0, 300000000, 9, updates=upd)
+    np.testing.assert_array_equal(hop_a, ora.hop)
+    np.testing.assert_array_equal(par_a, ora.parent)

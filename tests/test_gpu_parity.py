@@ -58,6 +58,12 @@ def test_gpu_matches_reference_golden(name):
         np.testing.assert_array_equal(net.delivered(), z["hop"] >= 0)
         np.testing.assert_array_equal(trim_zeros([r.relays for r in rounds]), trim_zeros(z["round_relays"]))
         assert net.message_count_send == int(z["round_relays"].sum())
+        # arrivals: sum over peers of message_count_recv (nodeconnection.py:215), duplicates
+        # included, churn-lost sends not
+        assert sum(r.received for r in rounds) == int(z["total_recv"])
+        assert rounds[0].received == 0
+        for a, b in zip(rounds, rounds[1:]):
+            assert b.received <= a.relays and (b.received == a.relays or int(z["churn_threshold"]))
     ora = oracle_for(z["rowptr"], z["colidx"], z["src"], mode, int(z["fanout"]), int(z["gossip_seed"]),
                      int(z["churn_threshold"]), int(z["churn_seed"]))
     assert_rounds_equal(rounds, ora.rounds)
