@@ -174,7 +174,9 @@ struct p2pg_engine {
   // run's first rounds (latency-bound sparse rounds) instead of leading it.  P2PG_SEEN_SPARE=0,
   // a plane above 1/16 of the device or a failed allocation: the reset zeroes seen in stream
   // order (spare_ready).
-  bool seen_spare_on = true;
+  bool seen_spare_on = true;    // P2PG_SEEN_SPARE (for good)
+  bool seen_spare_off = false;  // the current plane size / free memory ruled it out (re-examined
+                                // when the state is allocated again, alloc_state)
   uint64_t* seen_spare = nullptr;
   bool spare_pending = false;   // a zeroing of seen_spare is queued on `side` (ev_spare marks it)
   hipStream_t side = nullptr;
@@ -610,6 +612,7 @@ int alloc_state(p2pg_engine* e) {
   e->v_thresh = e->v_thresh_env >= 0.0 ? e->v_thresh_env : e->W <= 32 ? 0.95 : 0.3;
   s.M = e->M;
   e->plane_bytes = (size_t)e->V * e->W * sizeof(uint64_t);
+  e->seen_spare_off = false;  // a new plane size: the spare's size / memory check runs again
   e->bm_bytes = (size_t)((e->V + 31) / 32) * sizeof(uint32_t);
   const bool gossip = e->cfg.mode == P2PG_MODE_GOSSIP;
   const bool rec = (e->cfg.flags & P2PG_FLAG_RECORD) != 0;
@@ -927,7 +930,7 @@ const SeedStats& seed_stats(p2pg_engine* e) {
 // p2pg_reset's spare seen plane (p2pg_engine::seen_spare): allocated on first use; false when
 // disabled or when the device has no room for it (then it stays disabled)
 bool spare_ready(p2pg_engine* e) {
-  if (!e->seen_spare_on) return false;
+  if (!e->seen_spare_on || e->seen_spare_off) return false;
   if (e->seen_spare) return true;
   // only where it is cheap: a plane of at most 1/16 of the device (config 4: 5.1 GB of 288) with
   // room to spare, so that the copy never takes the memory a larger run (config 5's 51 GB planes,
@@ -936,7 +939,7 @@ bool spare_ready(p2pg_engine* e) {
   if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || e->plane_bytes > total_b / 16 ||
       free_b < 4 * e->plane_bytes) {
     (void)hipGetLastError();
-    e->seen_spare_on = false;
+    e->seen_spare_off = true;
     return false;
   }
   if (!e->side) {
@@ -944,14 +947,14 @@ bool spare_ready(p2pg_engine* e) {
         hipEventCreateWithFlags(&e->ev_spare, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&e->ev_main, hipEventDisableTiming) != hipSuccess) {
       (void)hipGetLastError();
-      e->seen_spare_on = false;
+      e->seen_spare_off = true;
       return false;
     }
   }
   if (hipMalloc((void**)&e->seen_spare, e->plane_bytes) != hipSuccess) {
     (void)hipGetLastError();
     e->seen_spare = nullptr;
-    e->seen_spare_on = false;
+    e->seen_spare_off = true;
     return false;
   }
   e->spare_pending = false;

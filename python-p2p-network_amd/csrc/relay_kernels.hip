@@ -2682,10 +2682,10 @@ hipError_t launch_gossip_scatter(const DevGraph& g, const DevState& st, const Ro
     return launch_wide_push_e(g, st, p, big_items, n_big, wide_big, n_wide_big, s);
   }
   // wider packed rows: the push-only mode of the one-peer-per-wave fused kernel, hubs by atomics
-  static const bool push_fused = [] {  // P2PG_PUSH_FUSED=0: one wave per source (A/B)
-    const char* e = std::getenv("P2PG_PUSH_FUSED");
-    return !(e && std::strcmp(e, "0") == 0);
-  }();
+  // P2PG_PUSH_FUSED=0: one wave per source (A/B; read per launch -- one per run -- so a test can
+  // switch it between engines of one process)
+  const char* pf_env = std::getenv("P2PG_PUSH_FUSED");
+  const bool push_fused = !(pf_env && std::strcmp(pf_env, "0") == 0);
   if (store_e && push_fused && st.W <= 64 && st.AW[p.round & 1] != nullptr && hubs_ok && !g.gid) {
 #define P2PG_FUSED_PO(CH, KK)                                                                       \
   hipLaunchKernelGGL((k_gossip_fused<CH, KK, 1>),                                                 \

@@ -106,6 +106,10 @@ def _c5_partitioned(g, src, thr, per_rank, record=False):
         t.start()
     for t in th:
         t.join(timeout=800)
+    stuck = [r for r, t in enumerate(th) if t.is_alive()]
+    if stuck:
+        shared["barrier"].abort()  # unblock the other rank; the stuck engine cannot be closed here
+        raise AssertionError(f"rank(s) {stuck} of the {C5_WORLD}-rank partition did not finish in 800 s")
     if errors:
         raise errors[0]
     return out

@@ -103,3 +103,34 @@ def test_new_sources_and_resets_recount_round_zero():
                 rows = _rows(net.run())
                 assert rows == ref[name][0], name
                 np.testing.assert_array_equal(net.seen_plane(), ref[name][1], err_msg=name)
+
+
+@pytest.mark.parametrize("M", [1536, 2560, 4096])  # W = 24 / 40 / 64: packed rows (AW planes)
+def test_partial_frontier_rows_every_push_form(M, monkeypatch):
+    """Inside p2pg_run, updates and the last dense pull write only the nonzero words of their
+    frontier rows (store_f == 2: the rows are valid under their AW masks only).  Every reader of
+    those rows -- the sparse push list, the per-source scatter, the fused push-only pass -- must
+    read them through AW: whole-row writes (P2PG_PARTIAL_F=0) give identical rounds and seen
+    planes, in each push form (default, unfused per-source scatter, per-source sparse push)."""
+    from p2pnetwork.gpu import PeerGraph, make_sources
+    g = PeerGraph.barabasi_albert(400_000, 4, seed=12)
+    src = make_sources(g.V, M, seed=13)
+    forms = {"auto": {}, "no_push_fused": {"P2PG_PUSH_FUSED": "0"},
+             "per_source_sparse": {"P2PG_SPARSE_LP": "0"}}
+    ref = None
+    for name, env in forms.items():
+        for partial in ("1", "0"):
+            for k in ("P2PG_PUSH_FUSED", "P2PG_SPARSE_LP"):
+                monkeypatch.delenv(k, raising=False)
+            for k, v in env.items():
+                monkeypatch.setenv(k, v)
+            monkeypatch.setenv("P2PG_PARTIAL_F", partial)
+            with _net(g, 0) as net:
+                net.broadcast(src)
+                rows = _rows(net.run())
+                seen = net.seen_plane()
+            if ref is None:
+                ref = (rows, seen)
+                continue
+            assert [r[:-1] for r in rows] == [r[:-1] for r in ref[0]], (name, partial)
+            np.testing.assert_array_equal(seen, ref[1], err_msg=f"{name} partial={partial}")
