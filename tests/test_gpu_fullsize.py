@@ -64,10 +64,11 @@ def config5_run(config5):
         net.broadcast(src)
         a = net.run()
         pop = np.zeros(g.V, dtype=np.int64)  # |seen set| per peer, 64 words at a time
-        cols, dig = {}, {}
+        cols, dig, whole = {}, {}, {}
         for w in range(len(src) // 64):
             col = net.seen_word(w)
             pop += np.bitwise_count(col)
+            whole[w] = _digest(col)
             for q in range(C5_WORLD):
                 dig[w, q] = _digest(col[bounds[q]:bounds[q + 1]])
             if w in (0, 63):
@@ -75,7 +76,7 @@ def config5_run(config5):
             del col
         net.reset()
         b = net.run()
-    return dict(rounds=a, rounds_again=b, pop=pop, cols=cols, dig=dig, bounds=bounds)
+    return dict(rounds=a, rounds_again=b, pop=pop, cols=cols, dig=dig, whole=whole, bounds=bounds)
 
 
 def _c5_partitioned(g, src, thr, per_rank, record=False):
@@ -168,6 +169,22 @@ def test_config5_full_size_flood_churn(config5, config5_run):
                       churn_seed=CSEED, record=False, want_seen=True)
     np.testing.assert_array_equal(ora.seen[:, 0], cols[63])
     assert_rounds_equal(rounds, ora.rounds)
+
+
+def test_config5_full_size_every_word_matches_oracle_digests(config5, config5_run):
+    """All 64 words of config 5's 4096-flood seen plane (100M peers, churn 0.05) == the C
+    oracle's 64-flood runs of their messages, which re-draw every churn decision (128-bit
+    digests made in the build container), and the additive per-round counters == the sums --
+    the whole plane pinned to the oracle in the default suite (node.py:106-120 with the lost
+    sends of nodeconnection.py:123-126).  Since the partitioned run is held to the same
+    per-rank digests of these columns above, it is pinned to the oracle too."""
+    from test_gpu_parity import assert_plane_matches_digests, plane_fixture
+    g, src, _ = config5
+    z = plane_fixture("plane_c5_ws100m_churn")
+    assert int(z["V"]) == g.V and int(z["M"]) == len(src)
+    whole = config5_run["whole"]  # the column digests taken as the plane was read
+    assert_plane_matches_digests(z, g, lambda w: np.frombuffer(whole[w], dtype=np.uint8),
+                                 config5_run["rounds"])
 
 
 def _c5_word_range():

@@ -240,7 +240,8 @@ def test_config3_flood_full_size_properties():
     assert sum(r.new_deliveries for r in sub) == int((hop >= 0).sum())
 
 
-C4_WORDS = (0, 9, 18, 27, 36, 45, 54, 63)  # spread over the 4096-broadcast row
+C4_WORDS = (0, 63)  # hop / parent against the C oracle run on the box; every word's seen column
+                    # is pinned by the oracle digests below
 
 
 @pytest.fixture(scope="module")
@@ -291,6 +292,60 @@ def test_config4_full_size_counters_are_the_sum_of_its_words(c4_full):
     for j, k in enumerate(keys):
         np.testing.assert_array_equal(trim_zeros(tot[:, j]), trim_zeros([getattr(r, k) for r in a]),
                                       err_msg=k)
+
+
+def plane_fixture(name):
+    """tests/golden/<name>.npz from tests/golden/make_plane_digests.py: the C oracle's per-word
+    seen-column digests and per-round counters for a full-size config (made in the build
+    container; no oracle runs on the GPU box)."""
+    from conftest import GOLDEN, load_golden
+    if not os.path.exists(os.path.join(GOLDEN, name + ".npz")):
+        pytest.skip(f"{name}.npz not generated (tests/golden/make_plane_digests.py)")
+    return load_golden(name)
+
+
+def csr_digest(g):
+    import xxhash
+    h = xxhash.xxh3_128()
+    h.update(np.ascontiguousarray(g.rowptr, dtype=np.int64))
+    h.update(np.ascontiguousarray(g.colidx, dtype=np.int32))
+    return np.frombuffer(h.digest(), dtype=np.uint8)
+
+
+def column_digest(col):
+    import xxhash
+    return np.frombuffer(xxhash.xxh3_128_digest(np.ascontiguousarray(col)), dtype=np.uint8)
+
+
+ORACLE_KEYS = ("new_deliveries", "relays", "active_vertices", "active_words", "wedges", "deg_active",
+               "scatter_words")  # oracle/coracle.py KEYS: the fixture's counter columns
+ADDITIVE = ("new_deliveries", "relays", "active_words", "wedges", "scatter_words")
+
+
+def assert_plane_matches_digests(z, g, digest_of, rounds):
+    """digest_of(w) -> the 128-bit digest of word w's seen column of the 4096-run (uint8 [16]);
+    rounds: its per-round counters.  Every
+    word == the oracle's 64-message run of those messages (128-bit digest), every additive
+    counter == the sum of the 64 oracle runs' (the graph itself pinned by its CSR digest)."""
+    np.testing.assert_array_equal(csr_digest(g), z["csr"], err_msg="generated graph differs")
+    bad = [w for w in range(len(z["word_dig"])) if not np.array_equal(digest_of(w), z["word_dig"][w])]
+    assert not bad, f"seen words {bad} differ from the C oracle"
+    tot = z["rounds"].sum(axis=0).astype(np.int64)
+    for k in ADDITIVE:
+        j = ORACLE_KEYS.index(k)
+        np.testing.assert_array_equal(trim_zeros(tot[:, j]), trim_zeros([getattr(r, k) for r in rounds]),
+                                      err_msg=k)
+
+
+def test_config4_full_size_every_word_matches_oracle_digests(c4_full):
+    """All 64 words of config 4's 4096-broadcast seen plane (10M peers) == the C oracle's 64-
+    broadcast runs of their messages, and the additive per-round counters == the sum of those
+    runs' -- the whole plane pinned to the oracle inside the default suite, by digests made in
+    the build container (node.py:114-120's relay, SURVEY.md A.3's picks)."""
+    g, src, seen, a, _ = c4_full
+    z = plane_fixture("plane_c4_ba10m_gossip")
+    assert int(z["V"]) == g.V and int(z["M"]) == len(src)
+    assert_plane_matches_digests(z, g, lambda w: column_digest(seen[:, w]), a)
 
 
 @pytest.mark.skipif(not os.environ.get("P2PG_FULL_ORACLE"),
