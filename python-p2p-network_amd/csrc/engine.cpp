@@ -56,10 +56,6 @@ struct p2pg_engine {
   int32_t* d_wide_big = nullptr;  // sources with deg > HUB_T (fused rounds' hub pushes)
   int64_t n_wide_big = 0;
   uint32_t* d_rev = nullptr;   // gossip: reverse edge slots
-  uint32_t* d_L = nullptr;     // light peers (deg <= LIGHT_DEG), one bit each (relay_light.hip)
-  int light_mode = -1;         // P2PG_LIGHT: -1 by the rule below, 0 never, 1 every fused round
-  double light_bits = 64.0;    // P2PG_LIGHT_BITS: a fused round is light when the round before had
-                               // at most this many first receipts per connected peer
   // pull hub split (deg > HUB_T)
   uint32_t* d_H = nullptr;
   int64_t* d_hub_items = nullptr;
@@ -279,7 +275,6 @@ void free_topology(p2pg_engine* e) {
   dfree(e->d_hub_big);
   dfree(e->d_wide_big);
   dfree(e->d_rev);
-  dfree(e->d_L);
   dfree(e->d_H);
   dfree(e->d_hub_items);
   dfree(e->d_hubs);
@@ -299,7 +294,6 @@ void free_graph(p2pg_engine* e) {
   dfree(e->d_hub_big);
   dfree(e->d_wide_big);
   dfree(e->d_rev);
-  dfree(e->d_L);
   dfree(e->d_H);
   dfree(e->d_hub_items);
   dfree(e->d_hubs);
@@ -343,7 +337,6 @@ RoundParams params(const p2pg_engine* e) {
   p.phase = -1;
   p.store_f = 1;
   p.dedup_push = 0;
-  p.light = nullptr;
   return p;
 }
 
@@ -543,15 +536,6 @@ bool part_dense(const p2pg_engine* e) {
          e->W > GROUPED_W_MAX && e->W <= 64;
 }
 
-// Is this fused round light (k_gossip_light takes the low-degree peers)?  By the first receipts
-// of the round before per connected peer (P2PG_LIGHT_BITS); config 4 at W = 64: rounds 11-13
-// and 22-23.  Only the kernel split depends on it, never a result.
-bool light_round(const p2pg_engine* e) {
-  if (e->light_mode == 0 || !e->d_L || e->d_gid || !gossip_light_supported(e->st)) return false;
-  if (e->light_mode == 1) return true;
-  return (double)e->last_new <= e->light_bits * (double)e->v_conn;
-}
-
 // Run this round's update and its (dense) pushes in one pass?
 bool update_push_round(const p2pg_engine* e, const RoundParams& p) {
   if (e->update_push == 0 || e->cfg.mode != P2PG_MODE_GOSSIP || e->push_mode != 0 || e->d_gid ||
@@ -708,8 +692,6 @@ int p2pg_create(const p2pg_config* cfg, p2pg_engine** out) {
   if (const char* f = std::getenv("P2PG_RUN_BATCH")) e->batch_rounds = std::atoi(f);
   if (const char* f = std::getenv("P2PG_DECAY_PRED")) e->decay_pred = std::strcmp(f, "0") != 0;
   if (const char* f = std::getenv("P2PG_PARTIAL_F")) e->partial_f = std::strcmp(f, "0") != 0;
-  if (const char* f = std::getenv("P2PG_LIGHT")) e->light_mode = std::atoi(f);
-  if (const char* f = std::getenv("P2PG_LIGHT_BITS")) e->light_bits = std::atof(f);
   if (const char* f = std::getenv("P2PG_SEEN_SPARE")) e->seen_spare_on = std::strcmp(f, "0") != 0;
   if (const char* m = std::getenv("P2PG_GOSSIP_PUSH"))
     e->push_mode = !std::strcmp(m, "atomic") ? 1 : (!std::strcmp(m, "store") ? 2 : 0);
@@ -844,13 +826,6 @@ int upload_graph(p2pg_engine* e, int64_t V, const int64_t* rowptr, const int32_t
     }
     HIPCHK(e, hipMalloc((void**)&e->d_H, sizeof(uint32_t) * H.size()));
     HIPCHK(e, hipMemcpy(e->d_H, H.data(), sizeof(uint32_t) * H.size(), hipMemcpyHostToDevice));
-    std::vector<uint32_t> L((V + 31) / 32, 0u);  // light peers: 1 <= deg <= LIGHT_DEG
-    for (int64_t v = 0; v < V; ++v) {
-      const int64_t d = rowptr[v + 1] - rowptr[v];
-      if (d >= 1 && d <= LIGHT_DEG) L[v >> 5] |= 1u << (v & 31);
-    }
-    HIPCHK(e, hipMalloc((void**)&e->d_L, sizeof(uint32_t) * (L.empty() ? 1 : L.size())));
-    if (!L.empty()) HIPCHK(e, hipMemcpy(e->d_L, L.data(), sizeof(uint32_t) * L.size(), hipMemcpyHostToDevice));
     if (!hubs.empty()) {
       HIPCHK(e, hipMalloc((void**)&e->d_hubs, sizeof(int32_t) * hubs.size()));
       HIPCHK(e, hipMalloc((void**)&e->d_hub_items, sizeof(int64_t) * items.size()));
@@ -1149,14 +1124,7 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
       // a frontier nobody observes is not stored: inside p2pg_run (not its last allowed
       // round), without hop/parent records
       p.store_f = (e->skip_frontier && !s.hop) ? 0 : 1;
-      // light round (few first receipts per peer the round before): the low-degree peers one
-      // lane each (k_gossip_light), the others through the fused kernel
-      if (light_round(e)) p.light = e->d_L;
-      if ((rc = timed(e, 7, [&] {
-             hipError_t r = launch_fused_round(e, g, p);
-             return r != hipSuccess || !p.light ? r : launch_gossip_light(g, s, p, e->stream);
-           })))
-        return rc;
+      if ((rc = timed(e, 7, [&] { return launch_fused_round(e, g, p); }))) return rc;
     } else {
       if ((rc = timed(e, 5, [&] {
              hipError_t r = launch_gossip_pull(g, s, p, e->hp, e->stream);

@@ -1724,7 +1724,7 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
     if (t < 0) return;
     // PO: the active peers; UP: the touched ones; else the saturated ones
     pf_s = PO ? st.A[cur][t] : UP ? st.T[cur][t] : st.S[t];
-    pf_h = (g.H ? g.H[t] : 0u) | (MODE == 0 && p.light ? p.light[t] : 0u);  // (light: k_gossip_light's)
+    pf_h = g.H ? g.H[t] : 0u;
     const int64_t u0 = t << 5;
     pf_rp = (lane <= 32 && u0 + lane <= V) ? (uint32_t)g.rowptr[u0 + lane] : 0u;
   };
