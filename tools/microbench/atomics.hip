@@ -37,6 +37,18 @@ __global__ void scat_read(const uint64_t* __restrict__ buf, uint64_t R, uint64_t
   for (uint64_t i = t; i < n; i += nt) { uint32_t h = hash32((uint32_t)i); uint64_t r = h % R; acc |= buf[r * 64 + (hash32(h) & 63)]; }
   if (acc == 0x123456789ull) out[0] = acc;
 }
+// the same with the old value consumed (a returning atomic: what a push-time dedup would need)
+__global__ void scat_atomic_or_ret(uint64_t* __restrict__ buf, uint64_t R, uint64_t n, uint64_t* out) {
+  uint64_t acc = 0;
+  uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x, nt = gridDim.x * (uint64_t)blockDim.x;
+  for (uint64_t i = t; i < n; i += nt) { uint32_t h = hash32((uint32_t)i); uint64_t r = h % R; acc += atomicOr((unsigned long long*)&buf[r * 64 + (hash32(h) & 63)], 1ull << (i & 63)); }
+  if (acc == 0x123456789ull) out[0] = acc;
+}
+// plain scattered 8 B stores (one lane, one random row: a lane-per-peer E-row writer)
+__global__ void scat_store(uint64_t* __restrict__ buf, uint64_t R, uint64_t n) {
+  uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x, nt = gridDim.x * (uint64_t)blockDim.x;
+  for (uint64_t i = t; i < n; i += nt) { uint32_t h = hash32((uint32_t)i); uint64_t r = h % R; buf[r * 64 + (hash32(h) & 63)] = i; }
+}
 // sequential streaming read for calibration
 __global__ void seq_read(const uint4* __restrict__ buf, uint64_t n16, uint4* out) {
   uint4 acc = {0,0,0,0};
@@ -65,6 +77,8 @@ int main() {
   uint64_t n = 200000000ull;
   timeit("scat_read 8B", n * 8.0, [&] { scat_read<<<blocks, threads>>>(buf, R, n, out); });
   timeit("scat_atomic_or 8B", n * 8.0, [&] { scat_atomic_or<<<blocks, threads>>>(buf, R, n); });
+  timeit("scat_atomic_or_ret 8B", n * 8.0, [&] { scat_atomic_or_ret<<<blocks, threads>>>(buf, R, n, out); });
+  timeit("scat_store 8B", n * 8.0, [&] { scat_store<<<blocks, threads>>>(buf, R, n); });
   for (int occ : {2, 4, 8, 32}) {
     char nm[64]; snprintf(nm, 64, "row_read grid=%dx256", 256 * occ);
     timeit(nm, items * 512.0, [&] { row_read<<<256 * occ, threads>>>(buf, R, items, out); });
