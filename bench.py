@@ -494,8 +494,11 @@ def main():
         "whole_step_frac_survey_model": sb_step / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBPS,
         "kernel_time_frac_of_step": kernel_ms_total / (elapsed / args.steps * 1e3),
         "relays_per_step": relays // args.steps,
-        # arrivals (sum of message_count_recv, nodeconnection.py:215): relays less churn losses
+        # arrivals (sum of message_count_recv, nodeconnection.py:215): relays less churn losses;
+        # a churn run counts its losses only with count_received (a counting pass per round,
+        # not part of the relay): there the sends of each round before, as an upper bound
         "received_per_step": sum(r.received for r in last),
+        "received_exact": all(r.received_exact for r in last),
         "relays_per_step_per_gpu": relays / args.steps / world,
         "exchange_ms_per_step": (net.exchange_s * 1e3) if partitioned else 0.0,
         # compacted exchange: fraction of the boundary rows that had a non-zero word and travelled

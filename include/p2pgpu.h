@@ -71,6 +71,12 @@ extern "C" {
                                     connection pushes for local connections, row pushes for
                                     ghost ones, exchanged); narrower rows: row atomics only */
 
+#define P2PG_FLAG_RECEIVED 16u /* churn runs: count every round's lost sends, so that
+                                    p2pg_round_stats.received is exact (a counting pass over the
+                                    round's frontier after each round: config 5 +100 %); without
+                                    it a churn run reports the sends of the round before there
+                                    (an upper bound, received_exact = 0)                     */
+
 typedef struct p2pg_engine p2pg_engine;
 typedef struct p2pg_graph p2pg_graph;
 
@@ -98,7 +104,8 @@ typedef struct p2pg_round_stats {
   uint64_t scatter_words;    /* gossip: nonzero (sender, target, word) masks pushed       */
   uint64_t touched_words;    /* gossip: nonzero pushed-to words consumed in round r       */
   int32_t push_form;         /* gossip: how round r's pushes left (P2PG_PUSH_*); flood 0    */
-  int32_t reserved_;
+  int32_t received_exact;    /* 1: `received` is exact; 0: a churn run without
+                                P2PG_FLAG_RECEIVED, `received` = the sends of round r-1     */
   uint64_t received;         /* packets that arrived in round r: the sends of round r-1 less
                                 those lost to churn or to a connection removed in between
                                 (sum over peers of message_count_recv += 1,

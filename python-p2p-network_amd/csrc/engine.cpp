@@ -556,8 +556,13 @@ int check_scatter_list(p2pg_engine* e, unsigned long long listed) {
   return P2PG_OK;
 }
 
-// Arrivals (p2pg_round_stats.received): a churn run counts the lost sends of every round.
-bool count_lost_on(const p2pg_engine* e) { return e->cfg.churn_threshold != 0; }
+// Arrivals (p2pg_round_stats.received): a churn run with P2PG_FLAG_RECEIVED counts the lost sends
+// of every round.
+bool count_lost_on(const p2pg_engine* e) {
+  return e->cfg.churn_threshold != 0 && (e->cfg.flags & P2PG_FLAG_RECEIVED);
+}
+// Is the `received` counter exact (no churn, or churn losses counted)?
+bool received_exact(const p2pg_engine* e) { return e->cfg.churn_threshold == 0 || count_lost_on(e); }
 
 // Enqueue the count of round r's lost sends (k_sends, count mode) over gs (the graph the sends
 // leave on; gone slots = removed connections) and gp (the graph round r's arrivals travelled
@@ -1282,7 +1287,7 @@ int p2pg_step(p2pg_engine* e, p2pg_round_stats* out) {
                      : fused_round ? P2PG_PUSH_FUSED
                      : up_round ? P2PG_PUSH_UPDATE_EDGE
                      : e->last_push_e ? P2PG_PUSH_EDGE : P2PG_PUSH_ATOMIC;
-    out->reserved_ = 0;
+    out->received_exact = received_exact(e) ? 1 : 0;
     out->received = e->round == 0 ? 0 : e->sent_last - e->lost_last;
   }
   e->sent_last = tot[ST_RELAYS];
@@ -1395,7 +1400,7 @@ static int run_decay_batch(p2pg_engine* e, int32_t R, p2pg_round_stats* out, int
     o.scatter_words = tot[ST_SCATTER];
     o.touched_words = tot[ST_AUX];
     o.push_form = P2PG_PUSH_ATOMIC;
-    o.reserved_ = 0;
+    o.received_exact = received_exact(e) ? 1 : 0;
     o.received = e->round == 0 ? 0 : e->sent_last - e->lost_last;
     e->sent_last = tot[ST_RELAYS];
     e->lost_last = 0;  // (no churn in a batched run)

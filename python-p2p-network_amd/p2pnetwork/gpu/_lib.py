@@ -19,6 +19,7 @@ FLAG_RECORD = 1
 FLAG_TIMING = 2
 FLAG_NO_AUTOSTOP = 4
 FLAG_LOCAL_GRAPH = 8
+FLAG_RECEIVED = 16
 
 # graph kinds of p2pg_graph_generate
 GRAPH_RANDOM_REGULAR = 0
@@ -60,7 +61,7 @@ class RoundStatsC(ctypes.Structure):
         ("scatter_words", ctypes.c_uint64),
         ("touched_words", ctypes.c_uint64),
         ("push_form", ctypes.c_int32),
-        ("reserved_", ctypes.c_int32),
+        ("received_exact", ctypes.c_int32),
         ("received", ctypes.c_uint64),
     ]
 

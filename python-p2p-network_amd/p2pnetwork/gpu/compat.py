@@ -240,6 +240,7 @@ class CompatNetwork:
         self._deg = graph.degree()
         self._pending = {}   # {(min, max): (connect?, dialler, other)} for the next round boundary
         make = engine_factory or GraphNetwork
+        engine_kw.setdefault("count_received", True)  # (small graphs: the churn count is cheap)
         self.engine = make(graph, mode=mode, fanout=fanout, gossip_seed=gossip_seed,
                            churn_threshold_value=churn_threshold_value, churn_seed=churn_seed,
                            **engine_kw)

@@ -48,10 +48,13 @@ class RoundStats:
     received: int = 0   # packets that arrived this round (sum of message_count_recv += 1,
                         # nodeconnection.py:215): last round's sends less the lost ones
     push_form: int = 0  # gossip: how this round's pushes left (PUSH_FORMS); not a result
+    received_exact: int = 1  # 0: a churn run without count_received -- `received` is then the
+                             # sends of the round before (an upper bound)
 
     @classmethod
     def from_c(cls, s):
-        return cls(*(int(getattr(s, f)) for f in STAT_FIELDS), push_form=int(s.push_form))
+        return cls(*(int(getattr(s, f)) for f in STAT_FIELDS), push_form=int(s.push_form),
+                   received_exact=int(s.received_exact))
 
     @classmethod
     def from_c_array(cls, buf, n):
@@ -108,7 +111,7 @@ def churn_threshold(p_drop):
 _ROUND_DTYPE = np.dtype([(n, {ctypes.c_int32: "<i4", ctypes.c_uint64: "<u8"}[t])
                          for n, t in _lib.RoundStatsC._fields_])
 assert _ROUND_DTYPE.itemsize == ctypes.sizeof(_lib.RoundStatsC)
-_ROUND_COLS = list(STAT_FIELDS) + ["push_form"]
+_ROUND_COLS = list(STAT_FIELDS) + ["push_form", "received_exact"]
 
 
 class GraphNetwork:
@@ -116,7 +119,8 @@ class GraphNetwork:
 
     def __init__(self, graph, mode="flood", fanout=3, gossip_seed=0x5EED, churn=0.0,
                  churn_threshold_value=None, churn_seed=0xC0FFEE, record=False, timing=False,
-                 device=0, msg_id_base=0, callback=None, autostop=True, local_graph=False):
+                 device=0, msg_id_base=0, callback=None, autostop=True, local_graph=False,
+                 count_received=False):
         if not isinstance(graph, PeerGraph):
             raise TypeError("graph must be a PeerGraph")
         if mode not in ("flood", "gossip"):
@@ -136,7 +140,8 @@ class GraphNetwork:
         cfg.msg_id_base = int(msg_id_base)
         cfg.flags = ((_lib.FLAG_RECORD if record else 0) | (_lib.FLAG_TIMING if timing else 0)
                      | (0 if autostop else _lib.FLAG_NO_AUTOSTOP)
-                     | (_lib.FLAG_LOCAL_GRAPH if local_graph else 0))
+                     | (_lib.FLAG_LOCAL_GRAPH if local_graph else 0)
+                     | (_lib.FLAG_RECEIVED if count_received else 0))
         cfg.device = int(device)
         self.config = cfg
         L = _lib.lib()

@@ -382,7 +382,8 @@ class PartitionedNetwork:
             g = self._round0_stats()
             g.scatter_words = int(tot[STAT_FIELDS[2:].index("scatter_words")])
         else:
-            g = RoundStats(st.round, int(tot[0] > 0), *[int(x) for x in tot])
+            g = RoundStats(st.round, int(tot[0] > 0), *[int(x) for x in tot],
+                           received_exact=st.received_exact)
         self.rounds.append(g)
         return g
 

@@ -27,7 +27,8 @@ def _bits(w, M):
 
 class MockEngine:
     def __init__(self, graph, mode="flood", fanout=3, gossip_seed=0, churn_threshold_value=0,
-                 churn_seed=0, record=False, timing=False, device=0, autostop=True, local_graph=False):
+                 churn_seed=0, record=False, timing=False, device=0, autostop=True, local_graph=False,
+                 count_received=False):
         self.g, self.mode, self.k = graph, mode, fanout
         self.gseed, self.thr, self.cseed = gossip_seed, churn_threshold_value, churn_seed
         self.V = graph.V

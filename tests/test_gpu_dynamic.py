@@ -25,7 +25,7 @@ def make_net(z, record=True, graph=None):
     g = graph if graph is not None else PeerGraph(z["rowptr"], z["colidx"])
     return GraphNetwork(g, mode=str(z["mode"]), fanout=int(z["fanout"]), gossip_seed=int(z["gossip_seed"]),
                         churn_threshold_value=int(z["churn_threshold"]), churn_seed=int(z["churn_seed"]),
-                        record=record)
+                        record=record, count_received=True)
 
 
 def oracle_of(z, updates=None):

@@ -48,7 +48,7 @@ def test_gpu_matches_reference_golden(name):
     z = load_golden(name)
     mode = str(z["mode"])
     net = gpu_net(z, mode, int(z["fanout"]), int(z["gossip_seed"]), int(z["churn_threshold"]),
-                  int(z["churn_seed"]))
+                  int(z["churn_seed"]), count_received=True)
     with net:
         net.broadcast(z["src"])
         rounds = net.run()
@@ -61,7 +61,7 @@ def test_gpu_matches_reference_golden(name):
         # arrivals: sum over peers of message_count_recv (nodeconnection.py:215), duplicates
         # included, churn-lost sends not
         assert sum(r.received for r in rounds) == int(z["total_recv"])
-        assert rounds[0].received == 0
+        assert rounds[0].received == 0 and all(r.received_exact for r in rounds)
         for a, b in zip(rounds, rounds[1:]):
             assert b.received <= a.relays and (b.received == a.relays or int(z["churn_threshold"]))
     ora = oracle_for(z["rowptr"], z["colidx"], z["src"], mode, int(z["fanout"]), int(z["gossip_seed"]),
