@@ -97,6 +97,44 @@ def test_compat_mock_engine_matches_reference_golden(name):
     assert net.explicit_packets == 0  # the dedup relay is carried by the engine alone
 
 
+@pytest.mark.parametrize("name", [n for n in golden_cases() if "gossip" in n])
+def test_compat_mock_harness_gossip_app_matches_reference_golden(name):
+    """The fixtures' own gossip app (send_to_node on the Philox-chosen connections) is
+    recognised as the engine's relay on the stand-in engine too."""
+    z = load_golden(name)
+    hop, par, sends, recv, net = run_compat(z, MockEngine, app=harness_gossip_app())
+    check(z, hop, par, sends, recv)
+    assert net.explicit_packets == 0
+
+
+def test_compat_explicit_sends_outside_deliveries():
+    """send_to_node outside a delivery is a one-connection origination (node.py:114-120),
+    NodeConnection.send is one packet without a counter (nodeconnection.py:107-160), an exclude
+    list makes a broadcast explicit, and an empty str packet stops its connection's stream for
+    good (the eot_pos > 0 loop, nodeconnection.py:211)."""
+    from p2pnetwork.gpu import PeerGraph
+    from p2pnetwork.gpu.compat import CompatNetwork, SimNode
+    got = []
+
+    class Rec(SimNode):
+        def node_message(self, node, data):
+            got.append((self.id, node.id, data))
+
+    g = PeerGraph.from_edges(4, [(0, 1), (0, 2), (0, 3)])
+    net = CompatNetwork(g, Rec, engine_factory=MockEngine)
+    n0 = net.nodes[0]
+    n0.send_to_node(net.connection(0, 2), {"p": 1})          # counted, one packet
+    net.connection(0, 3).send("raw")                        # not counted
+    n0.send_to_nodes({"q": 2}, exclude=[net.connection(0, 1)])  # explicit broadcast to 2, 3
+    net.nodes[1].send_to_node(net.connection(1, 0), "")      # empty packet: wedges 1 -> 0
+    net.nodes[1].send_to_node(net.connection(1, 0), "after")  # never delivered
+    net.run()
+    assert got == [("2", "0", {"p": 1}), ("2", "0", {"q": 2}), ("3", "0", "raw"), ("3", "0", {"q": 2})]
+    assert [n.message_count_send for n in net.nodes] == [1 + 2, 2, 0, 0]
+    assert [n.message_count_recv for n in net.nodes] == [0, 0, 2, 2]
+    assert net.explicit_packets == 6
+
+
 def _run_app(name, factory=None):
     """An app_* fixture's app on CompatNetwork: its node_message events and counters."""
     from p2pnetwork.gpu.compat import CompatNetwork, SimNode
