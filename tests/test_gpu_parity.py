@@ -270,6 +270,9 @@ def test_config4_full_size_reset_identical(c4_full):
         assert r.relays == 3 * r.new_deliveries
 
 
+@pytest.mark.skipif(not os.environ.get("P2PG_C4_SUM_OF_WORDS"),
+                    reason="64 one-word engines at 10M peers (~90 s); the oracle digests below pin the "
+                           "same plane and counter sums: P2PG_C4_SUM_OF_WORDS=1")
 def test_config4_full_size_counters_are_the_sum_of_its_words(c4_full):
     """Broadcasts are independent bit lanes: each of the 64 words of the 4096-run equals a
     64-broadcast run of its messages (global ids via msg_id_base, so the same Philox streams)
