@@ -106,13 +106,16 @@ __global__ __launch_bounds__(256, P2PG_GROUPED_WAVES) void k_gossip_fused_groupe
   const uint32_t* __restrict__ Ap = st.A[prv];
   const uint64_t* __restrict__ AWp = st.AW[prv];
   // packed E rows (sender's active words only, positions from AW) when AW planes exist --
-  // W > PACK_W_MAX_PLAIN; narrower rows are stored whole, zeros included, so that a receiver
-  // needs no random 8 B read of the sender's word mask per connection
-  const bool packed = AWp != nullptr;
+  // W > PACK_W_MAX_PLAIN, i.e. LW >= 4 (the launcher checks it); narrower rows are stored whole,
+  // zeros included, so that a receiver needs no random 8 B read of the sender's word mask per
+  // connection.  A compile-time fact: one gather path per instance.
+  constexpr bool packed = LW > 3;
+  static_assert((1 << 3) == PACK_W_MAX_PLAIN, "packed <=> LW > 3 needs PACK_W_MAX_PLAIN == 8");
   const int k = K > 0 ? K : p.fanout;
   const int gl = lane >> LW;        // this lane's batch peer
   const int wl = lane & (WP - 1);   // this lane's word
   const bool wvalid = wl < W;
+  const uint32_t below_wl = (1u << wl) - 1u;  // this lane's lower words (wl < 32)
   const uint64_t fm = wvalid ? full_mask(wl, W, st.M) : 0ull;
   const uint64_t gmask = (1ull << WP) - 1ull;
   const int64_t ntasks = (V + 31) >> 5;
@@ -206,13 +209,17 @@ __global__ __launch_bounds__(256, P2PG_GROUPED_WAVES) void k_gossip_fused_groupe
         const int idx = ok ? __builtin_ctzll(mg) : 0;
         mg &= mg - 1ull;
         bool here = ok;
-        int pos = wl;
-        if (packed) {  // uniform branch
-          const uint64_t a = bperm64(idx, amv);  // the sender's active-word mask
-          here = ok && ((a >> wl) & 1ull);
-          pos = __popcll(a & ((1ull << wl) - 1ull));
+        uint32_t pos = (uint32_t)wl;
+        if constexpr (packed) {
+          // the sender's active-word mask: W <= 32 words, its low half
+          const uint32_t a = bperm(idx, (uint32_t)amv);
+          here = ok && ((a >> wl) & 1u);
+          pos = (uint32_t)__popc(a & below_wl);
         }
-        X[qq] = here ? __builtin_nontemporal_load(&Src[(int64_t)(cb + (uint32_t)idx) * W + pos]) : 0ull;
+        // slot ids and W fit 32 bits: one 32 x 32 -> 64 multiply-add per address (an int64
+        // product took two v_mad_u64_u32 and two moves per gather)
+        const uint64_t* row = Src + (uint64_t)(cb + (uint32_t)idx) * (uint32_t)W;
+        X[qq] = here ? __builtin_nontemporal_load(row + pos) : 0ull;
       }
     };
     auto active_slots = [&](const GStage& q, uint32_t cb, int32_t v, bool rcv, uint32_t aword) -> uint64_t {
@@ -260,7 +267,7 @@ __global__ __launch_bounds__(256, P2PG_GROUPED_WAVES) void k_gossip_fused_groupe
               churn_dropped((uint32_t)p.round, gidx(g, u0 + q.b0 + o), gidx(g, tv), p.churn_thr,
                             p.cseed_lo, p.cseed_hi))
             x = 0ull;
-          st_row(&Eo[(int64_t)rv * W + (packed ? __popc(wmk & ((1u << wl) - 1u)) : wl)], x);
+          st_row(Eo + (uint64_t)rv * (uint32_t)W + (packed ? __popc(wmk & below_wl) : wl), x);
           if (x) c[ST_SCATTER] += 1;
         }
       }
@@ -474,11 +481,17 @@ hipError_t launch_lw(int lw, const DevGraph& g, const DevState& st, const RoundP
 
 }  // namespace
 
+// The instances' packed form is LW > 3: it must agree with the state's AW planes.
+static bool packed_ok(const DevState& st, int lw, int prv) {
+  return (lw > 3) == (st.AW[prv] != nullptr);
+}
+
 hipError_t launch_gossip_fused_grouped(const DevGraph& g, const DevState& st, const RoundParams& p,
                                        hipStream_t s) {
   if (st.W > 32 || st.W < 1) return hipErrorInvalidValue;
   int lw = 0;
   while ((1 << lw) < st.W) ++lw;
+  if (!packed_ok(st, lw, (p.round & 1) ^ 1)) return hipErrorInvalidValue;
   const bool ch = p.churn_thr != 0;
   if (p.fanout == 3) return ch ? launch_lw<true, 3>(lw, g, st, p, s) : launch_lw<false, 3>(lw, g, st, p, s);
   return ch ? launch_lw<true, 0>(lw, g, st, p, s) : launch_lw<false, 0>(lw, g, st, p, s);
@@ -489,6 +502,7 @@ hipError_t launch_gossip_push_grouped(const DevGraph& g, const DevState& st, con
   if (st.W > GROUPED_W_MAX || st.W < 1) return hipErrorInvalidValue;
   int lw = 0;
   while ((1 << lw) < st.W) ++lw;
+  if (!packed_ok(st, lw, p.round & 1)) return hipErrorInvalidValue;  // (PO: the round's own rows)
   const bool ch = p.churn_thr != 0;
   if (p.fanout == 3)
     return ch ? launch_lw<true, 3, true>(lw, g, st, p, s) : launch_lw<false, 3, true>(lw, g, st, p, s);
@@ -500,6 +514,7 @@ hipError_t launch_gossip_pull_grouped(const DevGraph& g, const DevState& st, con
   if (st.W > GROUPED_PULL_W_MAX || st.W < 1) return hipErrorInvalidValue;
   int lw = 0;
   while ((1 << lw) < st.W) ++lw;
+  if (!packed_ok(st, lw, (p.round & 1) ^ 1)) return hipErrorInvalidValue;
   // (no picks: the fanout template argument is irrelevant)
   return p.churn_thr != 0 ? launch_lw<true, 0, false, true>(lw, g, st, p, s)
                           : launch_lw<false, 0, false, true>(lw, g, st, p, s);
