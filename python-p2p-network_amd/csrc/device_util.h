@@ -136,6 +136,15 @@ __device__ __forceinline__ void st_frow(uint64_t* p, uint64_t x) {
 #endif
 }
 
+// Row r of a [rows][W] plane for a per-lane row id.  Row ids (peers, and E slots: rev[] holds
+// them as uint32) and W fit 32 bits, so the offset is one 32 x 32 -> 64 multiply-add per lane;
+// an int64 product takes two v_mad_u64_u32 and moves (the grouped kernel's gathers: W = 8 share
+// 67.8 -> 65.4 ms, profiles/r06/ab_grouped_addr.txt).
+template <class T>
+__device__ __forceinline__ T* at_row(T* plane, uint64_t r, int W) {
+  return plane + (uint64_t)(uint32_t)r * (uint32_t)W;
+}
+
 // Global peer id of a local vertex (partitioned runs keep ghosts in global-id order; the
 // Philox keys of churn and gossip are global ids so partitioning cannot change results).
 __device__ __forceinline__ uint32_t gidx(const DevGraph& g, int64_t x) {

@@ -67,7 +67,6 @@ struct GStage {
   uint32_t aword;     // ... the neighbour's activity word (round r-1) ...
   uint64_t amv;       // ... and its active-word mask
   bool rcv;           // slot exists and its owner peer is processed
-  uint64_t mr;        // lane (g, w): active slots of the first 64 not yet gathered
 };
 
 #ifndef P2PG_GROUPED_WAVES
@@ -202,26 +201,47 @@ __global__ __launch_bounds__(256, P2PG_GROUPED_WAVES) void k_gossip_fused_groupe
       for (int qq = 0; qq < GFG; ++qq) o |= X[qq];
       return o;
     };
-    auto gathers = [&](uint32_t cb, uint64_t& mg, uint64_t amv) {
+    // The active slots of one 64-slot window, compacted: lane r holds the r-th active slot's
+    // window index (cw_slot) and, packed, its sender's word mask (cw_am); a batch's slots are
+    // ordered by owner, so lane (g, w)'s peer owns entries [cw_base, cw_base + cw_cnt).  Gather k
+    // of a lane is then one ds_bpermute of entry cw_base + k -- a per-lane 64-bit slot mask
+    // (ctz, clear lowest, compare: ~9 VALU per gather) did the same walk before.  One window is
+    // live at a time: the first gathers of batch t+1 build it after batch t's last gathers.
+    uint32_t cw_slot = 0, cw_am = 0, cw_base4 = 0, cw_cnt = 0;
+    auto window = [&](uint64_t am, uint64_t amv, uint64_t ms, bool want) {
+      const bool act = (am >> lane) & 1ull;
+      const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(am >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)am, 0u));
+      // an inactive lane writes to entry 63, which is read only when all 64 slots are active
+      const int dst = (act ? (int)r : 63) << 2;
+      cw_slot = (uint32_t)__builtin_amdgcn_ds_permute(dst, lane);
+      if constexpr (packed) cw_am = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(uint32_t)amv);
+      const uint64_t below = ms & (0ull - ms);  // lowest slot of this lane's peer: entries before it
+      cw_base4 = (uint32_t)__popcll(am & (below - 1ull)) << 2;
+      cw_cnt = want ? (uint32_t)__popcll(am & ms) : 0u;
+    };
+    // gathers k0 .. k0 + GFG - 1 of this lane's peer in window cb
+    auto gathers = [&](uint32_t cb, uint32_t k0) {
 #pragma unroll
       for (int qq = 0; qq < GFG; ++qq) {
-        const bool ok = mg != 0ull;
-        const int idx = ok ? __builtin_ctzll(mg) : 0;
-        mg &= mg - 1ull;
+        const uint32_t k = k0 + (uint32_t)qq;
+        const bool ok = k < cw_cnt;
+        const int e4 = (int)(cw_base4 + (k << 2));
+        const uint32_t idx = (uint32_t)__builtin_amdgcn_ds_bpermute(e4, (int)cw_slot) & 63u;
         bool here = ok;
         uint32_t pos = (uint32_t)wl;
         if constexpr (packed) {
-          // the sender's active-word mask: W <= 32 words, its low half
-          const uint32_t a = bperm(idx, (uint32_t)amv);
+          // the sender's active-word mask: W <= 32 words
+          const uint32_t a = (uint32_t)__builtin_amdgcn_ds_bpermute(e4, (int)cw_am);
           here = ok && ((a >> wl) & 1u);
           pos = (uint32_t)__popc(a & below_wl);
         }
         // slot ids and W fit 32 bits: one 32 x 32 -> 64 multiply-add per address (an int64
         // product took two v_mad_u64_u32 and two moves per gather)
-        const uint64_t* row = Src + (uint64_t)(cb + (uint32_t)idx) * (uint32_t)W;
+        const uint64_t* row = Src + (uint64_t)(cb + idx) * (uint32_t)W;
         X[qq] = here ? __builtin_nontemporal_load(row + pos) : 0ull;
       }
     };
+    auto more = [&](uint32_t k0) { return __ballot(k0 < cw_cnt) != 0ull; };
     auto active_slots = [&](const GStage& q, uint32_t cb, int32_t v, bool rcv, uint32_t aword) -> uint64_t {
       bool act = rcv && ((aword >> (v & 31)) & 1u);
       if (CHURN && act) {
@@ -233,16 +253,15 @@ __global__ __launch_bounds__(256, P2PG_GROUPED_WAVES) void k_gossip_fused_groupe
       return __ballot(act);
     };
     auto first_gathers = [&](GStage& q) {
-      q.mr = 0;
 #pragma unroll
       for (int qq = 0; qq < GFG; ++qq) X[qq] = 0ull;
+      cw_cnt = 0;
       if (PO || q.n == 0) return;
       const uint64_t need = need_of(q);
       const uint64_t am = active_slots(q, q.rb0, q.v, q.rcv, q.aword);
       const uint64_t ms = my_slots(q, q.rb0);  // ds_bpermute: evaluated by every lane
-      uint64_t mg = need ? am & ms : 0ull;
-      gathers(q.rb0, mg, q.amv);
-      q.mr = mg;
+      window(am, q.amv, ms, need != 0ull);
+      gathers(q.rb0, 0u);
     };
 
     // ---- the flush of a consumed batch: lane = (slot, word), every active word of the slot's
@@ -281,9 +300,8 @@ __global__ __launch_bounds__(256, P2PG_GROUPED_WAVES) void k_gossip_fused_groupe
       const uint64_t need = need_of(a);
       if (PO) acc = a.s;  // the frontier row
       if (!PO) {
-        uint64_t mg = a.mr;
-        while (__ballot(mg != 0ull)) {
-          gathers(a.rb0, mg, a.amv);
+        for (uint32_t k0 = GFG; more(k0); k0 += GFG) {  // (the window of a's first gathers)
+          gathers(a.rb0, k0);
           acc |= x_or();
         }
         for (uint32_t cb = a.rb0 + 64; cb < a.rb1; cb += 64) {  // one peer wider than 64 slots
@@ -298,9 +316,9 @@ __global__ __launch_bounds__(256, P2PG_GROUPED_WAVES) void k_gossip_fused_groupe
           }
           const uint64_t am = active_slots(a, cb, v, own, aword);
           const uint64_t ms = my_slots(a, cb);
-          uint64_t m2 = need ? am & ms : 0ull;
-          while (__ballot(m2 != 0ull)) {
-            gathers(cb, m2, amv);
+          window(am, amv, ms, need != 0ull);
+          for (uint32_t k0 = 0; more(k0); k0 += GFG) {
+            gathers(cb, k0);
             acc |= x_or();
           }
         }

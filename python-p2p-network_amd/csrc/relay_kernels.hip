@@ -824,13 +824,13 @@ __global__ __launch_bounds__(256) void k_gossip_update1(DevGraph g, DevState st,
     q.x2 = 0;
     q.s2 = 0;
     const int64_t me = hl ? q.u2 : q.u;
-    if (me >= 0 && valid) q.x = nx[me * W + wl];
-    if (DUAL && q.u2 >= 0 && valid) q.x2 = nx[q.u2 * W + wl];
+    if (me >= 0 && valid) q.x = at_row(nx, me, W)[wl];
+    if (DUAL && q.u2 >= 0 && valid) q.x2 = at_row(nx, q.u2, W)[wl];
   };
   auto issue_s = [&](UpdStage& q) {
     const int64_t me = hl ? q.u2 : q.u;
-    if (me >= 0 && q.x) q.s = st.seen[me * W + wl];
-    if (DUAL && q.u2 >= 0 && q.x2) q.s2 = st.seen[q.u2 * W + wl];
+    if (me >= 0 && q.x) q.s = at_row(st.seen, me, W)[wl];
+    if (DUAL && q.u2 >= 0 && q.x2) q.s2 = at_row(st.seen, q.u2, W)[wl];
   };
 
   int64_t ct = -1;  // task of the consumed peers
@@ -847,14 +847,14 @@ __global__ __launch_bounds__(256) void k_gossip_update1(DevGraph g, DevState st,
     const uint64_t fan = p.mode == 0 ? (uint64_t)(deg > 0 ? deg - 1 : 0)
                                      : (uint64_t)(deg < p.fanout ? deg : p.fanout);
     if (x) {
-      st_prow(&nx[u * W + wl], 0ull);
+      st_prow(at_row(nx, u, W) + wl, 0ull);
       c[ST_AUX] += 1;  // touched (pushed-to) words consumed
     }
     const uint64_t nw = x & ~s;
     const uint64_t wm = PAIR ? (wm_all >> shift) & 0xFFFFFFFFull : wm_all;
     if (wm && st.AW[cur] && wl == 0) st.AW[cur][u] = wm;
-    if (nw) st_prow(&st.seen[u * W + wl], s | nw);
-    if (valid && wm && (p.store_f != 2 || nw)) st_prow(&Fc[u * W + wl], nw);  // (2: AW-valid rows)
+    if (nw) st_prow(at_row(st.seen, u, W) + wl, s | nw);
+    if (valid && wm && (p.store_f != 2 || nw)) st_prow(at_row(Fc, u, W) + wl, nw);  // (2: AW-valid rows)
     if (nw) {
       const uint64_t pc = (uint64_t)__popcll(nw);
       c[ST_NEW] += pc;
@@ -955,16 +955,16 @@ __global__ __launch_bounds__(256) void k_gossip_update_g(DevGraph g, DevState st
       const bool ok = peer && w < W;
       const int64_t u = (task << 5) + (peer ? select_bit32(tw, idx) : 0u);
       uint64_t x = 0, s = 0;
-      if (ok) x = nx[u * W + w];
+      if (ok) x = at_row(nx, u, W)[w];
       if (x) {
-        s = st.seen[u * W + w];
-        st_prow(&nx[u * W + w], 0ull);
+        s = at_row(st.seen, u, W)[w];
+        st_prow(at_row(nx, u, W) + w, 0ull);
         c[ST_AUX] += 1;  // touched (pushed-to) words consumed
       }
       const uint64_t nw = x & ~s;
       const uint64_t wm = (__ballot(nw != 0ull) >> (grp * WP)) & segm;  // this peer's new words
-      if (nw) st_prow(&st.seen[u * W + w], s | nw);
-      if (ok && wm) st_prow(&Fc[u * W + w], nw);
+      if (nw) st_prow(at_row(st.seen, u, W) + w, s | nw);
+      if (ok && wm) st_prow(at_row(Fc, u, W) + w, nw);
       if (wm) {
         const int64_t deg = g.rowptr[u + 1] - g.rowptr[u];
         // relays per first receipt: gossip min(k, deg); flood (rows materialized by a topology
@@ -1060,25 +1060,25 @@ __global__ __launch_bounds__(256) void k_gossip_update_gp(DevGraph g, DevState s
     // the rest of the task: its bits from the (take)-th on
     it_rest = take >= n ? 0u : it_rest & ~((1u << select_bit32(it_rest, take)) - 1u);
     if (q.me >= 0) {
-      if (wvalid) q.x = nx[(int64_t)q.me * W + w];
+      if (wvalid) q.x = at_row(nx, q.me, W)[w];
       q.r0 = (uint32_t)g.rowptr[q.me];
       q.r1 = (uint32_t)g.rowptr[q.me + 1];
     }
   };
   auto issue_s = [&](UpdStageG& q) {
-    if (q.me >= 0 && q.x) q.s = st.seen[(int64_t)q.me * W + w];
+    if (q.me >= 0 && q.x) q.s = at_row(st.seen, q.me, W)[w];
   };
   auto consume = [&](const UpdStageG& q) {
     const int64_t u = q.me;
     const uint64_t x = q.x, s = q.s;
     if (x) {
-      st_prow(&nx[u * W + w], 0ull);
+      st_prow(at_row(nx, u, W) + w, 0ull);
       c[ST_AUX] += 1;  // touched (pushed-to) words consumed
     }
     const uint64_t nw = x & ~s;
     const uint64_t wm = (__ballot(nw != 0ull) >> (grp * WP)) & segm;  // this peer's new words
-    if (nw) st_prow(&st.seen[u * W + w], s | nw);
-    if (q.me >= 0 && wvalid && wm) st_prow(&Fc[u * W + w], nw);
+    if (nw) st_prow(at_row(st.seen, u, W) + w, s | nw);
+    if (q.me >= 0 && wvalid && wm) st_prow(at_row(Fc, u, W) + w, nw);
     uint32_t bit = 0;
     if (wm) {
       const int64_t deg = (int64_t)(q.r1 - q.r0);
@@ -1438,10 +1438,10 @@ __device__ __forceinline__ void scatter_row(const DevGraph& g, const DevState& s
           (nbr0 + (jj < nn ? jj : 0)) << 2, (int)nbr);
       const uint64_t bal = __ballot(ok && x != 0ull);
       if (STORE_E && !(PART && (nj & REV_GHOST))) {
-        if (ok) st_row(&Eo[(int64_t)nj * W + rk_lane], x);
+        if (ok) st_row(at_row(Eo, nj, W) + rk_lane, x);
       } else {
         const int64_t u = (int64_t)(PART ? nj & ~REV_GHOST : nj);
-        if (x) atomicOr((unsigned long long*)&nx[u * W + sl * 64 + wc], (unsigned long long)x);
+        if (x) atomicOr((unsigned long long*)at_row(nx, u, W) + sl * 64 + wc, (unsigned long long)x);
         if (rk_lane == 0 && ((bal >> (lane & ~(seg - 1))) & segm))
           atomicOr(&Tn[u >> 5], 1u << (u & 31));
       }

@@ -101,7 +101,7 @@ __global__ __launch_bounds__(256) void k_sparse_words(DevGraph g, DevState st, R
         if (AWc) {
           am = AWc[u];
         } else {  // W <= PACK_W_MAX_PLAIN: the nonzero words of the row
-          for (int w = 0; w < W; ++w) am |= (uint64_t)(Fc[u * W + w] != 0ull) << w;
+          for (int w = 0; w < W; ++w) am |= (uint64_t)(at_row(Fc, u, W)[w] != 0ull) << w;
         }
       }
       const uint32_t wc = (uint32_t)__popcll(am);
@@ -207,7 +207,7 @@ __global__ __launch_bounds__(256) void k_sparse_push(DevGraph g, DevState st, Ro
       w = (uint32_t)(x & 63u);
       rb = g.rowptr[u];
       deg = (uint32_t)(g.rowptr[u + 1] - rb);
-      f = Fc[u * W + w];
+      f = at_row(Fc, u, W)[w];
     }
     const uint32_t bc = (uint32_t)__popcll(f);
     const uint32_t binc = wave_scan_u32(bc);
@@ -277,10 +277,10 @@ __global__ __launch_bounds__(256) void k_sparse_push(DevGraph g, DevState st, Ro
             continue;
           pushed += 1;  // a distinct (sender, target, word) mask, counted before the dedup
           if (p.dedup_push) {
-            mask &= ~st.seen[(int64_t)v * W + gw];
+            mask &= ~at_row(st.seen, v, W)[gw];
             if (!mask) continue;  // a duplicate in its entirety: nothing to deliver
           }
-          atomicOr((unsigned long long*)&nx[(int64_t)v * W + gw], (unsigned long long)mask);
+          atomicOr((unsigned long long*)at_row(nx, v, W) + gw, (unsigned long long)mask);
           touched[v] = 1u;  // a plain byte store: a T-bitmap atomic here doubled the atomics
         }
       }
@@ -421,7 +421,7 @@ __global__ __launch_bounds__(256) void k_wide_push(DevGraph g, DevState st, Roun
           if (CHURN && churn_dropped((uint32_t)p.round, gv, gidx(g, g.colidx[slot]), p.churn_thr,
                                      p.cseed_lo, p.cseed_hi))
             continue;  // a lost send: the connection's row stays zero
-          old[q] = atomicOr((unsigned long long*)&Eo[(int64_t)g.rev[slot] * W + epos], 1ull << b);
+          old[q] = atomicOr((unsigned long long*)at_row(Eo, g.rev[slot], W) + epos, 1ull << b);
         }
         // the returned words are used only after all picks are issued (one wait, not k)
         for (uint32_t q = 0; q < (K > 0 ? (uint32_t)K : k); ++q) pushed += old[q] == 0ull ? 1u : 0u;
