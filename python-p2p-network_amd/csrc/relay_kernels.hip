@@ -31,6 +31,14 @@
 
 // Dense pushes: the folded-round Philox of one source's draws (philox_pick); 0 = the generic
 // philox4x32_10 per draw (A/B builds)
+// scatter_row<.., DIRECT>: a slice with at most one new bit per word takes its picks lane = word,
+// without the compacted list (P2PG_PICK_DIRECT=0: always the list; A/B).  Taken by the fused
+// kernel's first-dense-round modes (push-only, update + push): c4 round 10 7.4 -> 6.9 ms; in the
+// fused rounds proper the extra path cost more in the peak rounds than it saved in the light
+// ones (211.2 -> 211.9 ms per step, profiles/r06/ab_pick_direct.txt)
+#ifndef P2PG_PICK_DIRECT
+#define P2PG_PICK_DIRECT 1
+#endif
 #ifndef P2PG_PICK_FOLD
 #define P2PG_PICK_FOLD 1
 #endif
@@ -1270,7 +1278,7 @@ __device__ __forceinline__ void tbl_clear(ScatterLds& L, int j, int w) {
 // PART (vertex-partitioned gossip ranks, STORE_E): a receiver slot marked REV_GHOST is a ghost's
 // connection -- the mask goes into the ghost's row push (next[r+1] row + T bit, exchanged after the
 // round) as in a sparse round, every other one into its E slot.
-template <bool CHURN, int K, bool STORE_E, int PH = 0, bool PART = false, class CT>
+template <bool CHURN, int K, bool STORE_E, int PH = 0, bool PART = false, bool DIRECT = false, class CT>
 __device__ __forceinline__ void scatter_row(const DevGraph& g, const DevState& st,
                                             const RoundParams& p, ScatterLds& L, int lane,
                                             int64_t v, int64_t rb, int64_t deg, int chunk,
@@ -1294,26 +1302,28 @@ __device__ __forceinline__ void scatter_row(const DevGraph& g, const DevState& s
   // the source's folded Philox rounds (philox_pick: only the message varies per draw)
   const PickKey pkey = pick_key((uint32_t)p.round, gv, p.gseed_lo, p.gseed_hi);
 
+  // Philox + Floyd for one (word, bit) entry e = word << 6 | bit of this slice, its picks ORed
+  // into the LDS table (an empty mask when !ok); CHECK: picks outside this chunk are dropped.
+  auto one = [&](auto check_v, uint32_t e, bool ok) {
+    constexpr bool CHECK = decltype(check_v)::value;
+    const uint32_t wl = e >> 6, bit = e & 63u;
+    const uint32_t mg = p.msg_base + (uint32_t)((sl * 64 + (int)wl) * 64) + bit;
+    uint32_t* const col = &L.tbl[tbl_entry_ix(e)];  // connection 0's (word, half)
+    const uint32_t mb = ok ? 1u << (bit & 31u) : 0u;
+    uint32_t pk[K > 0 ? K : 1];
+    if constexpr (P2PG_PICK_FOLD && K > 0 && K <= 4)
+      gossip_picks_k<K>(pkey, mg, (uint32_t)deg, pk);
+    else
+      gossip_picks_t<(K > 0 ? K : 1)>((uint32_t)p.round, gv, mg, (uint32_t)deg, p.gseed_lo,
+                                      p.gseed_hi, pk);
+#pragma unroll
+    for (int q = 0; q < (K > 0 ? K : 1); ++q) {
+      const uint32_t jj = pk[q] - (uint32_t)nb;
+      if (!CHECK || jj < (uint32_t)nn) atomicOr(col + jj * 128u, mb);
+    }
+  };
   // Philox + Floyd for list entries [0, n) of this wave, picks ORed into the LDS table.
   auto pick_batch = [&](auto check_v, uint32_t n) {
-    constexpr bool CHECK = decltype(check_v)::value;
-    auto one = [&](uint32_t e, bool ok) {
-      const uint32_t wl = e >> 6, bit = e & 63u;
-      const uint32_t mg = p.msg_base + (uint32_t)((sl * 64 + (int)wl) * 64) + bit;
-      uint32_t* const col = &L.tbl[tbl_entry_ix(e)];  // connection 0's (word, half)
-      const uint32_t mb = ok ? 1u << (bit & 31u) : 0u;
-      uint32_t pk[K > 0 ? K : 1];
-      if constexpr (P2PG_PICK_FOLD && K > 0 && K <= 4)
-        gossip_picks_k<K>(pkey, mg, (uint32_t)deg, pk);
-      else
-        gossip_picks_t<(K > 0 ? K : 1)>((uint32_t)p.round, gv, mg, (uint32_t)deg, p.gseed_lo,
-                                        p.gseed_hi, pk);
-#pragma unroll
-      for (int q = 0; q < (K > 0 ? K : 1); ++q) {
-        const uint32_t jj = pk[q] - (uint32_t)nb;
-        if (!CHECK || jj < (uint32_t)nn) atomicOr(col + jj * 128u, mb);
-      }
-    };
     // Strided: in batch b lane l takes entry l*nbat + b.  The list is word-major (a word's
     // bits are adjacent), so the 64 entries of a batch come from ~64 different words, i.e.
     // their table atomics hit different LDS banks.  The next batch's entry is read before this
@@ -1329,8 +1339,8 @@ __device__ __forceinline__ void scatter_row(const DevGraph& g, const DevState& s
       const uint32_t e0 = L.lst[i0 + b];
       const bool two = b + 1 < cnt;
       const uint32_t e1 = two ? L.lst[i0 + b + 1] : e0;
-      one(e0, true);
-      one(e1, two);
+      one(check_v, e0, true);
+      one(check_v, e1, two);
     }
 #else
     // Uniform trip count: a lane past its share evaluates a dummy entry whose table ORs carry
@@ -1340,7 +1350,7 @@ __device__ __forceinline__ void scatter_row(const DevGraph& g, const DevState& s
       const uint32_t e = en & 0x0FFFu;  // in range even when stale
       const uint32_t ni = i0 + b + 1;
       en = L.lst[ni < (uint32_t)GLIST ? ni : (uint32_t)GLIST - 1u];
-      one(e, b < cnt);
+      one(check_v, e, b < cnt);
     }
 #endif
   };
@@ -1380,12 +1390,29 @@ __device__ __forceinline__ void scatter_row(const DevGraph& g, const DevState& s
         tbl_clear(L, j, lane);
       }
     }
+    const uint32_t cnt = (uint32_t)__popcll(f);
+    // at most one new bit per word (light rounds: ~9 bits in ~8 words per peer): lane w's word
+    // is its own entry, one Philox batch with no list (the scan, the list writes and a sync cost
+    // more than the batch itself there)
+    bool direct = false;
+    if constexpr (DIRECT && K > 0 && P2PG_PICK_DIRECT) {
+      direct = __ballot(cnt > 1u) == 0ull;
+      if (direct) {
+        wave_lds_sync();  // (the table clear above, before the table atomics)
+        const uint32_t e = ((uint32_t)lane << 6) | (uint32_t)__builtin_ctzll(f | (1ull << 63));
+        if (nb == 0 && nn == (int)deg)
+          one(std::false_type{}, e, f != 0ull);
+        else
+          one(std::true_type{}, e, f != 0ull);
+        wave_lds_sync();
+        PROF_MARK(7);
+      }
+    }
     // word-major compaction: lane w lists its word's set bits at its exclusive prefix-sum
     // position (one DPP scan; a 32-bit ctz / clear per bit), so every lane gets an equal
     // share of the Philox work; pick_batch reads the list strided (distinct words per batch)
-    const uint32_t cnt = (uint32_t)__popcll(f);
-    const uint32_t incl = wave_scan_u32(cnt);
-    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    const uint32_t incl = direct ? 0u : wave_scan_u32(cnt);
+    const uint32_t total = direct ? 0u : (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     const uint32_t pos0 = incl - cnt;
     // a pass lists GLIST - 1 entries; the last list slot takes the entries not written
     constexpr uint32_t CAP = (uint32_t)GLIST - 1u;
@@ -2054,7 +2081,7 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
       if (PL) {
         // (no pushes: the sparse push that follows reads the frontier row)
       } else if (deg <= (uint64_t)GCHUNK) {
-        scatter_row<CHURN, K, true, 1, PART>(g, st, p, lds[wib], lane, u, a.beg, (int64_t)deg, 0, 0,
+        scatter_row<CHURN, K, true, 1, PART, PO || UP>(g, st, p, lds[wib], lane, u, a.beg, (int64_t)deg, 0, 0,
                                        nw, a.rv, 0, c PROF_PASS);
         pend = true;
         pu = u;
@@ -2064,7 +2091,7 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
         prcv = a.rv;
       } else if (deg <= 64) {
         for (int ch = 0; (int64_t)ch * GCHUNK < (int64_t)deg; ++ch)
-          scatter_row<CHURN, K, true, 0, PART>(g, st, p, lds[wib], lane, u, a.beg, (int64_t)deg, ch, 0,
+          scatter_row<CHURN, K, true, 0, PART, PO || UP>(g, st, p, lds[wib], lane, u, a.beg, (int64_t)deg, ch, 0,
                                       nw, a.rv, ch * GCHUNK, c PROF_PASS);
       } else {
         for (int ch = 0; (int64_t)ch * GCHUNK < (int64_t)deg; ++ch) {
@@ -2072,7 +2099,7 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
           const uint32_t j = a.beg + (uint32_t)(ch * GCHUNK - off) + lane;
           const uint32_t rvb = j < a.end ? g.rev[j] : 0u;
           __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-          scatter_row<CHURN, K, true, 0, PART>(g, st, p, lds[wib], lane, u, a.beg, (int64_t)deg, ch, 0,
+          scatter_row<CHURN, K, true, 0, PART, PO || UP>(g, st, p, lds[wib], lane, u, a.beg, (int64_t)deg, ch, 0,
                                       nw, rvb, off, c PROF_PASS);
         }
       }
