@@ -264,11 +264,11 @@ __device__ __forceinline__ uint64_t src_word_pair(const uint64_t* __restrict__ S
   if (__builtin_amdgcn_inverse_ballot_w64((uint64_t)h0 | ((uint64_t)h1 << 32))) {
     const bool lo = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) < 32u;
     const uint32_t pos = __builtin_amdgcn_mbcnt_hi(m1, __builtin_amdgcn_mbcnt_lo(lo ? m0 : 0u, 0u));
-    const uint32_t row = lo ? r0 : r1;
+    const uint32_t row = lo ? r0 : r1;  // (per lane: a 32 x 32 -> 64 address, at_row)
 #if P2PG_NT_LOADS
-    x = __builtin_nontemporal_load(&Src[(int64_t)row * W + pos]);
+    x = __builtin_nontemporal_load(at_row(Src, row, W) + pos);
 #else
-    x = Src[(int64_t)row * W + pos];
+    x = at_row(Src, row, W)[pos];
 #endif
   }
   return x;
