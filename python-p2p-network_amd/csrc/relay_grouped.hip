@@ -221,6 +221,9 @@ __global__ __launch_bounds__(256, P2PG_GROUPED_WAVES) void k_gossip_fused_groupe
     };
     // gathers k0 .. k0 + GFG - 1 of this lane's peer in window cb
     auto gathers = [&](uint32_t cb, uint32_t k0) {
+      // the window's first E row (wave-uniform); a gather's offset in the window is < 64 x W
+      // words, 32-bit: a scalar base and a 32-bit lane offset per load
+      const uint64_t* __restrict__ win = Src + (uint64_t)cb * (uint32_t)W;
 #pragma unroll
       for (int qq = 0; qq < GFG; ++qq) {
         const uint32_t k = k0 + (uint32_t)qq;
@@ -235,10 +238,11 @@ __global__ __launch_bounds__(256, P2PG_GROUPED_WAVES) void k_gossip_fused_groupe
           here = ok && ((a >> wl) & 1u);
           pos = (uint32_t)__popc(a & below_wl);
         }
-        // slot ids and W fit 32 bits: one 32 x 32 -> 64 multiply-add per address (an int64
-        // product took two v_mad_u64_u32 and two moves per gather)
-        const uint64_t* row = Src + (uint64_t)(cb + idx) * (uint32_t)W;
-        X[qq] = here ? __builtin_nontemporal_load(row + pos) : 0ull;
+        // (an int64 slot x width product per lane took two v_mad_u64_u32 and moves per gather)
+        const uint32_t ob = (idx * (uint32_t)W + pos) << 3;  // bytes: a scalar-base + lane-offset load
+        X[qq] = here ? __builtin_nontemporal_load(
+                           reinterpret_cast<const uint64_t*>(reinterpret_cast<const char*>(win) + ob))
+                     : 0ull;
       }
     };
     auto more = [&](uint32_t k0) { return __ballot(k0 < cw_cnt) != 0ull; };
