@@ -244,10 +244,11 @@ __device__ __forceinline__ uint64_t src_word_m(const uint64_t* __restrict__ Src,
   if (__builtin_amdgcn_inverse_ballot_w64(h)) {
     const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(am >> 32),
                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)am, 0u));
+    // (row is wave-uniform: a 32 x 32 -> 64 scalar product, at_row, instead of an int64 one)
 #if P2PG_NT_LOADS
-    x = __builtin_nontemporal_load(&Src[(int64_t)row * W + pos]);
+    x = __builtin_nontemporal_load(at_row(Src, row, W) + pos);
 #else
-    x = Src[(int64_t)row * W + pos];
+    x = at_row(Src, row, W)[pos];
 #endif
   }
   return x;
