@@ -424,7 +424,7 @@ __global__ __launch_bounds__(256, P2PG_PULL_WAVES) void k_pull1(DevGraph g, DevS
       const uint64_t nw = acc & need;
       const bool any = __ballot(nw != 0ull) != 0ull;
       if (nw) {
-        st_prow(&st.seen[u * W + lane], s1.s | nw);
+        st_prow(at_row(st.seen, u, W) + lane, s1.s | nw);
         const uint64_t pc = (uint64_t)__popcll(nw);
         const uint64_t per_bit = GOSSIP ? (deg < (uint64_t)p.fanout ? deg : (uint64_t)p.fanout)
                                         : deg - 1;
@@ -434,7 +434,7 @@ __global__ __launch_bounds__(256, P2PG_PULL_WAVES) void k_pull1(DevGraph g, DevS
         c[ST_WEDGES] += deg;
       }
       if (any) {
-        if (valid) st_prow(&Fc[u * W + lane], nw);
+        if (valid) st_prow(at_row(Fc, u, W) + lane, nw);
         aw |= 1u << s1.b;
         const uint64_t wm = __ballot(nw != 0ull);
         if (lane == 0) {
@@ -478,7 +478,7 @@ __global__ __launch_bounds__(256) void k_pull_hub_partial(DevGraph g, DevState s
     const int64_t rb = g.rowptr[u], re = g.rowptr[u + 1];
     const int64_t beg = rb + chunk * HUB_CHUNK;
     const int64_t end = beg + HUB_CHUNK < re ? beg + HUB_CHUNK : re;
-    const uint64_t need = valid ? fm & ~st.seen[u * W + lane] : 0ull;
+    const uint64_t need = valid ? fm & ~at_row(st.seen, u, W)[lane] : 0ull;
     uint64_t acc = 0;
     if (__ballot(need != 0ull) && !bit_test(st.S, u)) {
       for (int64_t cb = beg; cb < end; cb += 64) {
@@ -561,7 +561,7 @@ __global__ __launch_bounds__(256) void k_pull_hub_lds(DevGraph g, DevState st, R
     const int64_t rb = g.rowptr[u], re = g.rowptr[u + 1];
     const int64_t beg = rb + chunk * HUB_CHUNK;
     const int64_t end = beg + HUB_CHUNK < re ? beg + HUB_CHUNK : re;
-    const uint64_t need = valid ? fm & ~st.seen[u * W + lane] : 0ull;
+    const uint64_t need = valid ? fm & ~at_row(st.seen, u, W)[lane] : 0ull;
     // the same for every wave of the block (same hub): skip a saturated or full hub row
     const bool run = __ballot(need != 0ull) && !bit_test(st.S, u);
     if (tid == 0) s_n = 0u;
@@ -645,11 +645,11 @@ __global__ __launch_bounds__(256) void k_pull_hub_finalize(DevGraph g, DevState 
     uint64_t acc = 0;
     for (int64_t it = hp.item_begin[h]; it < hp.item_begin[h + 1]; ++it)
       acc |= hp.partial[it * 64 + lane];
-    const uint64_t s = valid ? st.seen[u * W + lane] : 0ull;
+    const uint64_t s = valid ? at_row(st.seen, u, W)[lane] : 0ull;
     const uint64_t nw = acc & fm & ~s;
     const uint64_t deg = (uint64_t)(g.rowptr[u + 1] - g.rowptr[u]);
     if (nw) {
-      st_prow(&st.seen[u * W + lane], s | nw);
+      st_prow(at_row(st.seen, u, W) + lane, s | nw);
       const uint64_t pc = (uint64_t)__popcll(nw);
       const uint64_t per_bit = GOSSIP ? (deg < (uint64_t)p.fanout ? deg : (uint64_t)p.fanout)
                                       : deg - 1;
@@ -1495,7 +1495,7 @@ __device__ __forceinline__ void scatter_row(const DevGraph& g, const DevState& s
       if (PART && (nj & REV_GHOST)) {  // a ghost's connection: its row push, exchanged
         const int64_t u = (int64_t)(nj & ~REV_GHOST);
         if (!dropped && bal) {
-          if (x) atomicOr((unsigned long long*)&nx[u * W + w], (unsigned long long)x);
+          if (x) atomicOr((unsigned long long*)at_row(nx, u, W) + w, (unsigned long long)x);
           if (lane == 0) {
             atomicOr(&Tn[u >> 5], 1u << (u & 31));
             c[ST_SCATTER] += (CT)__popcll(bal);
@@ -1506,9 +1506,9 @@ __device__ __forceinline__ void scatter_row(const DevGraph& g, const DevState& s
       // receiver-major: the row lands in the RECEIVER's slot for this connection, so the
       // pull streams its own contiguous slot range; packed: only the active words, in order
       if (st.AW[cur]) {
-        if (f) st_row(&Eo[(int64_t)nj * W + __popcll(fam & ((1ull << lane) - 1ull))], dropped ? 0ull : x);
+        if (f) st_row(at_row(Eo, nj, W) + __popcll(fam & ((1ull << lane) - 1ull)), dropped ? 0ull : x);
       } else if (valid) {
-        st_row(&Eo[(int64_t)nj * W + w], dropped ? 0ull : x);
+        st_row(at_row(Eo, nj, W) + w, dropped ? 0ull : x);
       }
       if (!dropped && lane == 0) c[ST_SCATTER] += (CT)__popcll(bal);
     } else {
@@ -1518,7 +1518,7 @@ __device__ __forceinline__ void scatter_row(const DevGraph& g, const DevState& s
       if (CHURN && churn_dropped((uint32_t)p.round, gv, gidx_s(g, u), p.churn_thr,
                                  p.cseed_lo, p.cseed_hi))
         continue;
-      if (x) atomicOr((unsigned long long*)&nx[u * W + w], (unsigned long long)x);
+      if (x) atomicOr((unsigned long long*)at_row(nx, u, W) + w, (unsigned long long)x);
       if (lane == 0) {
         atomicOr(&Tn[u >> 5], 1u << (u & 31));
         c[ST_SCATTER] += (CT)__popcll(bal);
@@ -1797,8 +1797,8 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
     if (q.u < 0) return;
     // PO: the peer's frontier row (its new receipts of this round) instead of its seen row;
     // UP: the seen row and, in the stage's mask field, the push row (the arrivals)
-    if (valid) q.s = ld_once(&(PO ? Fc : st.seen)[(int64_t)q.u * W + lane]);
-    if (UP) q.am = valid ? st.next[cur][(int64_t)q.u * W + lane] : 0ull;
+    if (valid) q.s = ld_once(at_row(PO ? Fc : st.seen, q.u, W) + lane);
+    if (UP) q.am = valid ? at_row(st.next[cur], q.u, W)[lane] : 0ull;
     // PO: the row's active-word mask (a frontier row written by the update may hold stale words
     // outside it, RoundParams::store_f == 2)
     if (PO) q.am = ldc(st.AW[cur] + q.u);
@@ -1962,7 +1962,7 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
     // the wait below covers them
     uint64_t remote = 0;
     if (PART && GATHER && ((ldc(st.T[cur] + (u >> 5)) >> (u & 31)) & 1u) && valid)
-      remote = ld_once(&st.next[cur][(int64_t)u * W + lane]);
+      remote = ld_once(at_row(st.next[cur], u, W) + lane);
     PROF_MARK(0);
     if (GATHER) {
       uint64_t m = a.mr;  // the rest of the first 64 slots, then further 64-slot chunks
@@ -2042,7 +2042,7 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
     if (HALF) acc |= bperm64(lane ^ 32, acc);  // lanes 32-63 gathered for words 0-31 too
     if (PART) acc |= remote;
     if (UP && acc) {  // the push row is consumed: all-zero again outside touched rows
-      st_prow(&st.next[cur][(int64_t)u * W + lane], 0ull);
+      st_prow(at_row(st.next[cur], u, W) + lane, 0ull);
       c[ST_AUX] += 1;  // touched (pushed-to) words consumed
     }
     flush_pending();
@@ -2055,7 +2055,7 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
     const uint64_t nw = PO ? ((a.am >> lane) & 1ull ? a.s : 0ull) : acc & need;
     const uint64_t wm = __ballot(nw != 0ull);
     if (!PO && nw) {
-      st_frow(&st.seen[u * W + lane], a.s | nw);
+      st_frow(at_row(st.seen, u, W) + lane, a.s | nw);
       const uint32_t pc = (uint32_t)__popcll(nw);
       const uint32_t kf = K > 0 ? (uint32_t)K : (uint32_t)p.fanout;
       const uint32_t per_bit = deg < (uint64_t)kf ? (uint32_t)deg : kf;
@@ -2066,7 +2066,7 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
     }
     if (wm) {
       if (!PO) {
-        if (valid && p.store_f && (p.store_f != 2 || nw)) st_frow(&Fc[u * W + lane], nw);
+        if (valid && p.store_f && (p.store_f != 2 || nw)) st_frow(at_row(Fc, u, W) + lane, nw);
         aw |= 1u << (u & 31);
         if (lane == 0) {
           st.AW[cur][u] = wm;
