@@ -142,7 +142,11 @@ __device__ __forceinline__ void st_frow(uint64_t* p, uint64_t x) {
 // 67.8 -> 65.4 ms, profiles/r06/ab_grouped_addr.txt).
 template <class T>
 __device__ __forceinline__ T* at_row(T* plane, uint64_t r, int W) {
-  return plane + (uint64_t)(uint32_t)r * (uint32_t)W;
+  // byte offset r x (W x 8): the row stride in bytes is kernel-constant, so the per-lane form is
+  // one v_mad_u64_u32 with the plane as its addend and the scalar form has no 64-bit shift
+  using B = typename std::conditional<std::is_const<T>::value, const char, char>::type;
+  const uint32_t stride = (uint32_t)W * (uint32_t)sizeof(T);
+  return reinterpret_cast<T*>(reinterpret_cast<B*>(plane) + (uint64_t)(uint32_t)r * stride);
 }
 
 // Global peer id of a local vertex (partitioned runs keep ghosts in global-id order; the

@@ -1864,23 +1864,22 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
     }
     // all slot ids / word masks first, then all FG loads back to back: a readlane between
     // two loads would make the wave wait for the first one (merged vmcnt state)
+    // (a slot past the last active one keeps am = 0: its load mask is empty, no select needed)
     uint32_t sv[FG];
     uint64_t am[FG];
-    bool ok[FG];
 #pragma unroll
     for (int k = 0; k < FG; ++k) {
       sv[k] = 0u;
       am[k] = 0ull;
-      ok[k] = m != 0ull;
       if (m) {
         const int idx = __builtin_ctzll(m);
-        m &= m - 1ull;
+        m &= ~(1ull << idx);
         sv[k] = q.beg + (uint32_t)idx;  // receiver-major E: the row of slot j is j
         am[k] = (uint64_t)readlane64((int64_t)q.am, idx);
       }
     }
 #pragma unroll
-    for (int k = 0; k < FG; ++k) X[k] = src_word_m(Src, sv[k], W, am[k], ok[k] ? am[k] & needm : 0ull);
+    for (int k = 0; k < FG; ++k) X[k] = src_word_m(Src, sv[k], W, am[k], am[k] & needm);
     mr = m;
   };
 
@@ -1998,14 +1997,12 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
         while (!HALF && m) {
           uint32_t sv[8];
           uint64_t am[8];
-          bool ok[8];
 #pragma unroll
           for (int k = 0; k < 8; ++k) {
-            ok[k] = m != 0ull;
-            am[k] = 0ull;
+            am[k] = 0ull;  // (past the last active slot: an empty load mask)
             if (m) {
               const int idx = __builtin_ctzll(m);
-              m &= m - 1ull;
+              m &= ~(1ull << idx);
               sv[k] = cb + (uint32_t)idx;  // the E row of slot cb + idx (receiver-major)
               am[k] = (uint64_t)readlane64((int64_t)sam, idx);
             } else {
@@ -2015,7 +2012,7 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
           uint64_t x[8];
 #pragma unroll
           for (int k = 0; k < 8; ++k)
-            x[k] = src_word_m(Src, sv[k], W, am[k], ok[k] ? am[k] & needm : 0ull);
+            x[k] = src_word_m(Src, sv[k], W, am[k], am[k] & needm);
 #pragma unroll
           for (int k = 0; k < 8; ++k) acc |= x[k];
         }
