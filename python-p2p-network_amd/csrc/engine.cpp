@@ -1021,6 +1021,8 @@ int p2pg_reset(p2pg_engine* e) {
   e->prev2_aw = e->prev2_av = e->prev2_new = 0;
   e->prev_sw = 0;
   e->saw_dense = false;
+  // (a previous run's unresolved launch timings belong to it, not to the next one)
+  e->ev_cls.clear();
   for (int i = 0; i < P2PG_KCLASS_N; ++i) {
     e->kms[i] = 0;
     e->klaunch[i] = 0;
@@ -2281,6 +2283,14 @@ int p2pg_restore(p2pg_engine* e, const void* buf, int64_t size) {
 
 int p2pg_kernel_times(p2pg_engine* e, double ms[P2PG_KCLASS_N], int64_t launches[P2PG_KCLASS_N]) {
   if (!e) return P2PG_ERR_ARG;
+  if (!e->ev_cls.empty()) {
+    // launches still unresolved: a run whose last rounds went without a counter read-back (a
+    // batched flood or decay tail) -- wait for them, so the sums cover every launch counted
+    HIPCHK(e, hipSetDevice(e->cfg.device));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    const int r = resolve_timings(e);
+    if (r) return r;
+  }
   for (int i = 0; i < P2PG_KCLASS_N; ++i) {
     if (ms) ms[i] = e->kms[i];
     if (launches) launches[i] = e->klaunch[i];

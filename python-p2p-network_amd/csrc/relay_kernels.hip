@@ -228,10 +228,10 @@ struct FusedStage {
 __device__ __forceinline__ uint64_t src_word(const uint64_t* __restrict__ Src, uint32_t row,
                                              int W, int lane, bool packed, uint64_t am,
                                              bool want) {
-  if (!packed) return want ? Src[(int64_t)row * W + lane] : 0ull;
+  if (!packed) return want ? at_row(Src, row, W)[lane] : 0ull;
   const bool here = want && ((am >> lane) & 1ull);
   const int pos = __popcll(am & ((1ull << lane) - 1ull));
-  return here ? Src[(int64_t)row * W + pos] : 0ull;
+  return here ? at_row(Src, row, W)[pos] : 0ull;
 }
 
 
@@ -389,7 +389,7 @@ __global__ __launch_bounds__(256, P2PG_PULL_WAVES) void k_pull1(DevGraph g, DevS
               am[k] = 0ull;
               if (m) {
                 const int idx = __builtin_ctzll(m);
-                m &= m - 1ull;
+                m &= ~(1ull << idx);
                 sv[k] = (uint32_t)__builtin_amdgcn_readlane((int)srow, idx);
                 if (packed) am[k] = (uint64_t)readlane64((int64_t)sam, idx);
               } else {
@@ -1844,13 +1844,13 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
         r0[k] = r1[k] = m0[k] = m1[k] = 0u;
         if (m) {
           const int i0 = __builtin_ctzll(m);
-          m &= m - 1ull;
+          m &= ~(1ull << i0);
           r0[k] = q.beg + (uint32_t)i0;
           m0[k] = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)q.am, i0);
         }
         if (m) {
           const int i1 = __builtin_ctzll(m);
-          m &= m - 1ull;
+          m &= ~(1ull << i1);
           r1[k] = q.beg + (uint32_t)i1;
           m1[k] = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)q.am, i1);
         }
@@ -1975,13 +1975,13 @@ __global__ __launch_bounds__(256, P2PG_FUSED_WAVES) void k_gossip_fused(DevGraph
             r0[k] = r1[k] = m0[k] = m1[k] = 0u;
             if (m) {
               const int i0 = __builtin_ctzll(m);
-              m &= m - 1ull;
+              m &= ~(1ull << i0);
               r0[k] = cb + (uint32_t)i0;
               m0[k] = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)sam, i0);
             }
             if (m) {
               const int i1 = __builtin_ctzll(m);
-              m &= m - 1ull;
+              m &= ~(1ull << i1);
               r1[k] = cb + (uint32_t)i1;
               m1[k] = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)sam, i1);
             }
